@@ -1,0 +1,207 @@
+"""Benchmark of the triangle raster hot path (BASELINE.json metric:
+"Mpixels/s shaded+Z-tested (and fps) ... 1M tris; 1/2/4/8 GPU").
+
+Workload: 3840x2160 RGB context, a 1,000,000-
+triangle displaced UV sphere (synthetic, deterministic), Gouraud shading,
+depth test LESS with write, both faces drawn.  One step = one frame:
+uniform clear + depth clear + DrawTriangleBuffer of the whole mesh, with the
+triangles already resident in HBM.  The work unit is a covered on-screen
+pixel x triangle pair (counted once, outside the timed region, by the
+library's fragment counter; equal to the oracle's count — tests check it).
+
+Multi-GPU (torchrun, one process per GPU): the frame's 32-pixel tile rows are
+owned round-robin by the ranks; every rank bins and rasterises only its rows
+(no data-path collective), then the owned rows are gathered to rank 0 over
+RCCL.  value = frame fragments / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+PEAK_HBM_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (W, H, kind, params)
+    "c3": dict(W=3840, H=2160, mesh=(500, 1000), gouraud=True, desc="C3: 1M-tri displaced UV sphere, 3840x2160, Gouraud, Z LESS+write"),
+    "c3_1080p": dict(W=1920, H=1080, mesh=(500, 1000), gouraud=True, desc="1M-tri displaced UV sphere, 1920x1080, Gouraud, Z LESS+write"),
+    "c2": dict(W=1920, H=1080, soup=(10000, 32.0, None), gouraud=False, desc="C2: 10k random opaque tris, 1920x1080, flat, Z LESS+write"),
+    "c5": dict(W=1920, H=1080, soup=(50000, 256.0, (0.2, 0.8)), gouraud=False, write=False,
+               desc="C5: 50k alpha-blended tris back-to-front, 1920x1080, Z test on, write off"),
+}
+
+
+def make_scene(cfg):
+    import scenes
+    if "mesh" in cfg:
+        xy, z, c = scenes.sphere_mesh(cfg["W"], cfg["H"], *cfg["mesh"])
+    else:
+        n, spread, alpha = cfg["soup"]
+        xy, z, c = scenes.triangle_soup(n, cfg["W"], cfg["H"], spread, seed=1234, alpha=alpha)
+        if alpha is not None:   # back-to-front
+            order = np.argsort(-z.mean(axis=1), kind="stable")
+            xy, z, c = xy[order], z[order], c[order]
+    return xy, z, c
+
+
+def algorithmic_bytes(cfg, n_tri):
+    """B = N_tri*S_tri + W*H*(8*ipp + 4*[Z written]),
+    S_tri = 104 B flat / 168 B Gouraud; ipp = 3 (RGB)."""
+    s_tri = 168 if cfg["gouraud"] else 104
+    zw = 4 if cfg.get("write", True) else 0
+    return n_tri * s_tri + cfg["W"] * cfg["H"] * (8 * 3 + zw)
+
+
+def cpu_baseline(cfg, xy, z, c, budget_s=10.0, max_frames=50):
+    """The oracle (CPU restatement, single thread) on the same frames."""
+    import scenes
+    f = scenes.OracleFactory()
+    times, frags = [], 0
+    ctx = f.context(cfg["W"], cfg["H"], False)
+    t_start = time.perf_counter()
+    while len(times) < max_frames and (time.perf_counter() - t_start < budget_s or len(times) < 2):
+        t0 = time.perf_counter()
+        ctx.set_color(0, 0, 0, 0)
+        ctx.set_depth_state(True, cfg.get("write", True))
+        ctx.clear_depth()
+        ctx.draw_triangles(xy, c, z=z)
+        times.append(time.perf_counter() - t0)
+        frags = ctx.last_fragment_count()
+    med = float(np.median(times))
+    return {"value": frags / med / 1e6, "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": f"{len(times)} full frames of the same workload, median {med*1e3:.1f} ms/frame "
+                      f"(oracle/oracle.c, gcc -O3 -ffp-contract=off, 1 thread)"}
+
+
+def load_pmc_traffic(cfg_name):
+    p = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        return d.get("hbm_bytes_per_launch"), d
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extra", action="store_true", help="also time c2/c5 and report them under 'extra'")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    R.set_device(local_rank)
+
+    cfg = CONFIGS[args.config]
+    W, H = cfg["W"], cfg["H"]
+    xy, z, c = make_scene(cfg)
+    n_tri = len(xy)
+    ctx = R.RenderContext(W, H, False)
+    buf = R.TriangleBuffer(xy, c, z=z, gouraud=cfg["gouraud"])
+
+    def frame():
+        ctx.set_color(0, 0, 0, 0)
+        ctx.set_depth_state(True, cfg.get("write", True))
+        ctx.clear_depth()
+        ctx.draw_triangle_buffer(buf)
+
+    # fragment count of one frame (outside the timed region)
+    ctx.set_fragment_counting(True)
+    frame()
+    ctx.flush()
+    frags = ctx.get_fragment_count()
+    ctx.set_fragment_counting(False)
+
+    for _ in range(args.warmup):
+        frame()
+    ctx.flush()
+    ctx.reset_kernel_timing()
+    ctx.enable_kernel_timing(True)
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    ctx.flush()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dist.barrier()
+    ctx.enable_kernel_timing(False)
+
+    ms = dt / args.steps * 1e3
+    kernels = {}
+    for name in ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "tile_raster", "fill"):
+        tot, cnt = ctx.get_kernel_timing(name)
+        if cnt:
+            kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
+    raster_us = kernels.get("tile_raster")
+    B = algorithmic_bytes(cfg, n_tri)
+    achieved = B / (raster_us * 1e-6) / 1e9 if raster_us else None
+    traffic, pmc = load_pmc_traffic(args.config)
+
+    if rank != 0:
+        return
+    result = {
+        "metric": "Mpixels/s shaded+Z-tested (and fps)",
+        "value": round(frags * args.steps / dt / 1e6, 1),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "fps": round(1e3 / ms, 1),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic displaced UV sphere / seeded soup, SURVEY.md §8d)",
+        "config": {"workload": cfg["desc"], "width": W, "height": H, "triangles": n_tri,
+                   "fragments_per_frame": int(frags), "frame_pixels": W * H,
+                   "parallelism": f"tile-row x{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
+                     "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None,
+                     "traffic": traffic,
+                     "kernel": "k_tile_raster", "algorithmic_bytes_per_launch": B,
+                     "frame_frac": round(B / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)},
+        "kernel_us": kernels,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        result["cpu_baseline"] = cpu_baseline(cfg, xy, z, c)
+        result["vs_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+    print(json.dumps(result))
+
+
+if __name__ == "__main__":
+    main()

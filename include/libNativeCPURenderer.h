@@ -1,0 +1,125 @@
+/*
+ * libNativeCPURenderer.h — C ABI of the MI355X (gfx950) raster library.
+ *
+ * Drop-in for the render part of the reference's ABI
+ * (/root/reference/src/libNativeCPURenderer.h:83-152): the same symbol names
+ * and parameter types (LP64: i64 = long, f64 = double, bool = C/C++ bool,
+ * handles are opaque pointers), so the reference's ctypes binding
+ * (libNativeCPURendererPybind.py) can load this .so unchanged for every raster
+ * call.  Each declaration cites the reference prototype it replaces as
+ * h:<line> and the implementation it restates as cpp:<lines>.
+ *
+ * Differences in behaviour: pixel data lives in HBM and draws
+ * are asynchronous kernel launches — readback calls (GetBuffer*, GetColor,
+ * GetDepthBuffer) and Flush are the sync points; Destroy* really free;
+ * CreateRenderContext returns NULL when no HIP device is usable (no CPU path).
+ * New entry points are additive and marked NEW.
+ */
+#ifndef LIBNATIVECPURENDERER_AMD_H
+#define LIBNATIVECPURENDERER_AMD_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef long i64;
+typedef double f64;
+typedef unsigned char iu8;
+
+typedef struct RenderContext RenderContext;   /* h:32-42 (opaque here) */
+typedef struct Texture Texture;               /* h:44-49 (opaque here) */
+typedef struct TriangleBuffer TriangleBuffer; /* NEW: device-resident triangle soup */
+
+/* ---- render context (cpp:3-45, 277-316) ---------------------------------- */
+i64 GetBufferSize(RenderContext* ctx);                                   /* h:84  */
+RenderContext* CreateRenderContext(i64 width, i64 height, bool enableAlpha); /* h:85 */
+void DestroyRenderContext(RenderContext* ctx);                           /* h:86  */
+void ResizeRenderContext(RenderContext* ctx, i64 width, i64 height);     /* h:149 */
+void SaveContextState(RenderContext* ctx);                               /* h:92  */
+bool RestoreContextState(RenderContext* ctx);                            /* h:93  */
+void GetBuffer(RenderContext* ctx, f64* buffer);                         /* h:94  */
+void GetBufferAsUInt8(RenderContext* ctx, iu8* buffer);                  /* h:95  */
+
+/* ---- textures (cpp:318-384, 950-988) ------------------------------------- */
+Texture* CreateTexture(i64 width, i64 height, bool enableAlpha, f64* buffer);      /* h:96  */
+Texture* CreateTextureUInt8(i64 width, i64 height, bool enableAlpha, iu8* buffer); /* h:97  */
+void DestroyTexture(Texture* tex);                                       /* h:98  */
+Texture* CreateTextureFromRenderContext(RenderContext* ctx);             /* h:99  */
+Texture* CreateTextureFromRenderContextShared(RenderContext* ctx);       /* h:148 */
+Texture* ResampleTexture(Texture* tex, i64 width, i64 height);           /* h:119 */
+i64 GetTextureWidth(Texture* tex);                                       /* h:120 */
+i64 GetTextureHeight(Texture* tex);                                      /* h:121 */
+bool GetTextureEnableAlpha(Texture* tex);                                /* h:122 */
+
+/* ---- transform / colour-transform state, host side (cpp:386-492, 623-641) */
+void SetTransform(RenderContext* ctx, f64 a, f64 b, f64 c, f64 d, f64 e, f64 f);   /* h:100 */
+void ApplyTransform(RenderContext* ctx, f64 a, f64 b, f64 c, f64 d, f64 e, f64 f); /* h:101 */
+void Scale(RenderContext* ctx, f64 sx, f64 sy);                          /* h:102 */
+void Translate(RenderContext* ctx, f64 tx, f64 ty);                      /* h:103 */
+void Rotate(RenderContext* ctx, f64 angle);                              /* h:104 */
+void TransformPoint(RenderContext* ctx, f64 x, f64 y, f64* out_x, f64* out_y); /* h:105 (inline in cpp:455; exported here) */
+void GetTransform(RenderContext* ctx, f64 out_matrix[6]);                /* h:106 */
+void GetInverseTransform(RenderContext* ctx, f64 out_matrix[6]);         /* h:107 */
+void SetColorTransform(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a);  /* h:110 */
+void ApplyColorTransform(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a); /* h:111 */
+
+/* ---- pixel ops and primitives (cpp:494-948, 1285-1316) ------------------- */
+bool SetPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a);   /* h:108 */
+bool ApplyPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a); /* h:109 (inline in cpp:515; exported here) */
+void SetColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a);           /* h:112 */
+void GetColor(RenderContext* ctx, f64 x, f64 y, f64* out_r, f64* out_g, f64* out_b, f64* out_a); /* h:113 */
+void FillColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a);          /* h:114 */
+void DrawTexture(RenderContext* ctx, Texture* tex, f64 x, f64 y, f64 width, f64 height); /* h:115 */
+void DrawRect(RenderContext* ctx, f64 x, f64 y, f64 width, f64 height, f64 r, f64 g, f64 b, f64 a); /* h:116 */
+void DrawLine(RenderContext* ctx, f64 x1, f64 y1, f64 x2, f64 y2, f64 width,
+              f64 r, f64 g, f64 b, f64 a);                               /* h:117 */
+void DrawCircle(RenderContext* ctx, f64 x, f64 y, f64 radius, f64 r, f64 g, f64 b, f64 a); /* h:118 */
+void DrawVerticalGrd(RenderContext* ctx, f64 x, f64 y, f64 width, f64 height,
+                     f64 top_r, f64 top_g, f64 top_b, f64 top_a,
+                     f64 bottom_r, f64 bottom_g, f64 bottom_b, f64 bottom_a); /* h:146 */
+void DrawSplittedTexture(RenderContext* ctx, Texture* tex, f64 x, f64 y, f64 width, f64 height,
+                         f64 uStart, f64 uEnd, f64 vStart, f64 vEnd);    /* h:147 */
+i64 GetVersion(void);                                                     /* h:143, =1 (h:9) */
+
+/* ---- NEW: triangles, depth, Gouraud (the north-star path) --
+ * xy: n*6 f64 (x0,y0,x1,y1,x2,y2) in user space (the context transform is
+ * applied); z: n*3 f64 depths in [0,1] or NULL; rgba: n*4 f64 flat colours,
+ * or n*12 per-vertex colours when gouraud. */
+void SetDepthState(RenderContext* ctx, bool test, bool write);           /* NEW: LESS test, write enable */
+void ClearDepth(RenderContext* ctx, uint32_t value);                     /* NEW: deferred, on-chip */
+void GetDepthBuffer(RenderContext* ctx, uint32_t* out);                  /* NEW: W*H u32, sync */
+void DrawTriangles(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba,
+                   i64 n, bool gouraud);                                  /* NEW: host arrays */
+void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba,
+                         i64 n, bool gouraud);                            /* NEW: device pointers */
+TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f64* rgba,
+                                     bool gouraud);                       /* NEW: one H2D upload */
+void DestroyTriangleBuffer(TriangleBuffer* tb);                          /* NEW */
+void DrawTriangleBuffer(RenderContext* ctx, TriangleBuffer* tb);         /* NEW */
+i64 GetTriangleBufferCount(TriangleBuffer* tb);                          /* NEW */
+void SetFragmentCounting(RenderContext* ctx, bool on);                   /* NEW: covered-fragment counter */
+i64 GetFragmentCount(RenderContext* ctx);                                /* NEW */
+
+/* ---- NEW: device, sync, interop, errors, measurement --------------------- */
+bool SetDevice(i64 device);                      /* device for objects created next on this thread */
+i64 GetDeviceCount(void);
+i64 GetContextDevice(RenderContext* ctx);
+void Flush(RenderContext* ctx);                  /* wait for every queued draw */
+void ResolvePending(RenderContext* ctx);         /* materialise deferred clears */
+void* GetDeviceBufferPtr(RenderContext* ctx);    /* framebuffer in HBM (RCCL / interop) */
+void* GetStreamPtr(RenderContext* ctx);          /* hipStream_t the context launches on */
+void GetBufferAsUInt8Device(RenderContext* ctx, iu8* dev_out); /* cpp:52-57 into HBM */
+void GetTextureBuffer(Texture* tex, f64* out);
+const char* GetLastErrorString(void);            /* "" when no HIP call failed */
+void ClearLastError(void);
+void EnableKernelTiming(RenderContext* ctx, bool on);
+bool GetKernelTiming(RenderContext* ctx, const char* name, f64* total_ms, i64* count);
+void ResetKernelTiming(RenderContext* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,106 @@
+"""ctypes signature table of the C ABI (include/libNativeCPURenderer.h).
+
+The reference's binding re-declares argtypes/restype inside every method
+(/root/reference/src/libNativeCPURendererPybind.py:51-300); here they are
+declared once per library from this table.  The table is pure data so the
+test-suite can apply the shared part of it to the CPU oracle as well.
+"""
+from __future__ import annotations
+
+import ctypes
+
+P = ctypes.c_void_p
+L = ctypes.c_long
+D = ctypes.c_double
+B = ctypes.c_bool
+U32 = ctypes.c_uint32
+
+# name -> (restype, argtypes).  "ref" = entry point of the reference ABI
+# (h:83-152); "new" = additive entry point of this library.
+REFERENCE_ABI = {
+    "GetBufferSize": (L, (P,)),
+    "CreateRenderContext": (P, (L, L, B)),
+    "DestroyRenderContext": (None, (P,)),
+    "ResizeRenderContext": (None, (P, L, L)),
+    "SaveContextState": (None, (P,)),
+    "RestoreContextState": (B, (P,)),
+    "GetBuffer": (None, (P, P)),
+    "GetBufferAsUInt8": (None, (P, P)),
+    "CreateTexture": (P, (L, L, B, P)),
+    "CreateTextureUInt8": (P, (L, L, B, P)),
+    "DestroyTexture": (None, (P,)),
+    "CreateTextureFromRenderContext": (P, (P,)),
+    "CreateTextureFromRenderContextShared": (P, (P,)),
+    "SetTransform": (None, (P, D, D, D, D, D, D)),
+    "ApplyTransform": (None, (P, D, D, D, D, D, D)),
+    "Scale": (None, (P, D, D)),
+    "Translate": (None, (P, D, D)),
+    "Rotate": (None, (P, D)),
+    "TransformPoint": (None, (P, D, D, P, P)),
+    "GetTransform": (None, (P, P)),
+    "GetInverseTransform": (None, (P, P)),
+    "SetPixel": (B, (P, L, L, D, D, D, D)),
+    "ApplyPixel": (B, (P, L, L, D, D, D, D)),
+    "SetColorTransform": (None, (P, D, D, D, D)),
+    "ApplyColorTransform": (None, (P, D, D, D, D)),
+    "SetColor": (None, (P, D, D, D, D)),
+    "GetColor": (None, (P, D, D, P, P, P, P)),
+    "FillColor": (None, (P, D, D, D, D)),
+    "DrawTexture": (None, (P, P, D, D, D, D)),
+    "DrawSplittedTexture": (None, (P, P, D, D, D, D, D, D, D, D)),
+    "DrawRect": (None, (P, D, D, D, D, D, D, D, D)),
+    "DrawLine": (None, (P, D, D, D, D, D, D, D, D, D)),
+    "DrawCircle": (None, (P, D, D, D, D, D, D, D)),
+    "DrawVerticalGrd": (None, (P, D, D, D, D, D, D, D, D, D, D, D, D)),
+    "ResampleTexture": (P, (P, L, L)),
+    "GetTextureWidth": (L, (P,)),
+    "GetTextureHeight": (L, (P,)),
+    "GetTextureEnableAlpha": (B, (P,)),
+    "GetVersion": (L, ()),
+}
+
+# triangles / depth (also exported by the oracle)
+TRIANGLE_ABI = {
+    "SetDepthState": (None, (P, B, B)),
+    "ClearDepth": (None, (P, U32)),
+    "GetDepthBuffer": (None, (P, P)),
+    "DrawTriangles": (None, (P, P, P, P, L, B)),
+}
+
+# HIP-library-only additions
+DEVICE_ABI = {
+    "DrawTrianglesDevice": (None, (P, P, P, P, L, B)),
+    "CreateTriangleBuffer": (P, (L, P, P, P, B)),
+    "DestroyTriangleBuffer": (None, (P,)),
+    "DrawTriangleBuffer": (None, (P, P)),
+    "GetTriangleBufferCount": (L, (P,)),
+    "SetFragmentCounting": (None, (P, B)),
+    "GetFragmentCount": (L, (P,)),
+    "GetLastErrorString": (ctypes.c_char_p, ()),
+    "ClearLastError": (None, ()),
+    "SetDevice": (B, (L,)),
+    "GetDeviceCount": (L, ()),
+    "GetContextDevice": (L, (P,)),
+    "Flush": (None, (P,)),
+    "ResolvePending": (None, (P,)),
+    "GetDeviceBufferPtr": (P, (P,)),
+    "GetStreamPtr": (P, (P,)),
+    "GetBufferAsUInt8Device": (None, (P, P)),
+    "GetTextureBuffer": (None, (P, P)),
+    "EnableKernelTiming": (None, (P, B)),
+    "GetKernelTiming": (B, (P, ctypes.c_char_p, P, P)),
+    "ResetKernelTiming": (None, (P,)),
+}
+
+HIP_LIBRARY_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **DEVICE_ABI}
+ORACLE_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, "OracleLastFragmentCount": (L, ())}
+
+
+def bind(lib: ctypes.CDLL, table: dict) -> ctypes.CDLL:
+    """Declares restype/argtypes of every entry of `table` on `lib`;
+    raises AttributeError naming the first missing export."""
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib

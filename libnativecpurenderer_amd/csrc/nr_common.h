@@ -1,0 +1,183 @@
+// nr_common.h — shared types and device helpers of the MI355X raster library.
+//
+// Every device helper restates one reference routine bit for bit
+// (/root/reference/src/libNativeCPURenderer.cpp:<lines> cited per helper).
+// The whole library is compiled with -ffp-contract=off: the reference build
+// has no FMA, so neither may we.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+#include <vector>
+#include <climits>
+
+typedef long i64;
+typedef double f64;
+typedef unsigned char iu8;
+typedef uint32_t u32;
+
+// ---------------------------------------------------------------------------
+// error latch (no exceptions cross the ABI; SURVEY §8b "Errors")
+// ---------------------------------------------------------------------------
+void nr_set_error(const char* where, hipError_t e);
+void nr_set_error_msg(const char* msg);
+#define NR_CHECK(call)                                              \
+    do {                                                            \
+        hipError_t nr_e_ = (call);                                  \
+        if (nr_e_ != hipSuccess) nr_set_error(#call, nr_e_);        \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// host objects
+// ---------------------------------------------------------------------------
+struct NRState { f64 m[6]; f64 ct[4]; };
+
+// Scratch of the triangle pipeline, grown on demand (never shrunk).
+typedef unsigned long long u64;
+struct TriScratch {
+    u64* cnt = nullptr; u64* off = nullptr; size_t tri_cap = 0;          // per triangle
+    u32* keys[2] = {nullptr, nullptr}; u32* vals[2] = {nullptr, nullptr}; size_t pair_cap = 0;
+    u32* tile_start = nullptr; u32* tile_end = nullptr; size_t tile_cap = 0;
+    void* temp = nullptr; size_t temp_bytes = 0;                        // hipcub scratch
+    u64* h_total = nullptr;                 // pinned readback: [0] pairs, [1] last count, [2] fragments
+    u64* d_frag = nullptr;                  // device fragment counter
+    f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
+};
+
+enum NRKernelId { NRK_TRI_COUNT = 0, NRK_TRI_SCAN, NRK_TRI_EMIT, NRK_TRI_SORT, NRK_TILE_RANGES,
+                  NRK_TILE_RASTER, NRK_PRIM, NRK_FILL, NRK_COUNT_ };
+
+struct RenderContext {
+    i64 width = 0, height = 0;
+    bool enableAlpha = false;
+    f64* buffer = nullptr;            // device, row-major interleaved, W*H*ipp (cpp:3-5)
+    f64 m[6] = {1, 0, 0, 1, 0, 0};    // transformMatrix (h:39)
+    f64 ct[4] = {1, 1, 1, 1};         // colorTransform (h:40)
+    std::vector<NRState> stack;       // stateStack (h:41)
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // depth (new)
+    u32* depth = nullptr;
+    bool depthTest = false, depthWrite = false;
+    // deferred clears: a uniform SetColor / ClearDepth is kept pending and
+    // consumed on chip by the tiled raster, or materialised before any
+    // other operation that touches the buffer.
+    bool pendColor = false; f64 pendColorValue = 0;
+    bool pendDepth = false; u32 pendDepthValue = 0xFFFFFFFFu;
+    TriScratch tri;
+    // per-kernel HIP-event timing (bench.py's live roofline measurement)
+    bool timing = false;
+    std::vector<hipEvent_t> evPool;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> evPending;
+    f64 kTimeMs[NRK_COUNT_] = {0};
+    i64 kCount[NRK_COUNT_] = {0};
+    // covered-fragment counting (the work count of the Mpixels/s metric)
+    bool countFragments = false;
+    bool fragPending = false;
+    u64 fragTotal = 0;
+};
+
+struct Texture {
+    i64 width = 0, height = 0;
+    bool enableAlpha = false;
+    f64* buffer = nullptr;            // device
+    bool owns = true;                 // false: alias of a context framebuffer (cpp:377-384)
+    RenderContext* aliasOf = nullptr;
+    int device = 0;
+};
+
+struct TriangleBuffer {
+    i64 n = 0;
+    bool gouraud = false;
+    f64* xy = nullptr;    // n*6   (x0,y0,x1,y1,x2,y2)
+    f64* z = nullptr;     // n*3 or null
+    f64* rgba = nullptr;  // n*4 (flat) or n*12 (Gouraud)
+    int device = 0;
+};
+
+// host helpers shared across translation units
+hipStream_t nr_stream_for(int device);
+void nr_materialize(RenderContext* ctx);          // flush pending clears
+void nr_materialize_color(RenderContext* ctx);
+void nr_materialize_depth(RenderContext* ctx);
+void nr_ensure_depth(RenderContext* ctx);
+void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
+void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);
+void nr_fill_f64(hipStream_t s, f64* p, i64 n, f64 v);
+void nr_fill_u32(hipStream_t s, u32* p, i64 n, u32 v);
+
+// x86-64 cvttsd2si semantics for (i64)double: out of range / NaN -> INT64_MIN
+static inline i64 nr_f2i64(f64 v) {
+    if (!(v >= -9223372036854775808.0 && v < 9223372036854775808.0)) return LONG_MIN;
+    return (i64)v;
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+// cpp:446-453, expression order kept: (m0*x + m2*y) + m4
+__host__ __device__ __forceinline__ void nr_xform(const f64* m, f64 x, f64 y, f64& ox, f64& oy) {
+    ox = m[0] * x + m[2] * y + m[4];
+    oy = m[1] * x + m[3] * y + m[5];
+}
+
+// cpp:515-549 body on an already-located pixel: colour transform, then "over"
+// unless a == 1; RGBA stores dst.a = a.
+__device__ __forceinline__ void nr_apply_pixel(f64* p, int ipp, f64 r, f64 g, f64 b, f64 a,
+                                               f64 ct0, f64 ct1, f64 ct2, f64 ct3) {
+    r *= ct0; g *= ct1; b *= ct2; a *= ct3;
+    if (a != 1) {
+        r = p[0] * (1 - a) + r * a;
+        g = p[1] * (1 - a) + g * a;
+        b = p[2] * (1 - a) + b * a;
+    }
+    p[0] = r; p[1] = g; p[2] = b;
+    if (ipp == 4) p[3] = a;
+}
+
+// cpp:555-573 nearest-texel sampler (clamp to [0,w-2]x[0,h-2]); alpha of an RGB
+// texture is uninitialised in the reference (Appendix A.2) and defined as 1.
+__device__ __forceinline__ void nr_sample(const f64* tb, i64 tw, i64 th, bool talpha, f64 x, f64 y,
+                                          f64& r, f64& g, f64& b, f64& a) {
+    if (x < 0) x = 0;
+    if (x >= (f64)(tw - 1)) x = (f64)(tw - 2);
+    if (y < 0) y = 0;
+    if (y >= (f64)(th - 1)) y = (f64)(th - 2);
+    i64 ipp = talpha ? 4 : 3;
+    i64 index = (i64)y * tw * ipp + (i64)x * ipp;
+    if (index < 0) index = 0;   // 1-px-wide textures read index -1 in the reference (UB)
+    r = tb[index + 0];
+    g = tb[index + 1];
+    b = tb[index + 2];
+    a = talpha ? tb[index + 3] : 1.0;
+}
+
+// cpp:822-845 even-odd crossing test
+template <int N>
+__device__ __forceinline__ bool nr_point_in_polygon(f64 x, f64 y, const f64 (&pts)[N][2]) {
+    int j = N - 1;
+    bool res = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if ((pts[i][1] > y) != (pts[j][1] > y) &&
+            (x < (pts[j][0] - pts[i][0]) * (y - pts[i][1]) / (pts[j][1] - pts[i][1]) + pts[i][0]))
+            res = !res;
+        j = i;
+    }
+    return res;
+}
+
+// depth quantisation (new)
+__host__ __device__ __forceinline__ u32 nr_quantize_depth(f64 z) {
+    if (!(z > 0.0)) return 0u;
+    if (z >= 1.0) return 0xFFFFFFFFu;
+    return (u32)(z * 4294967295.0);
+}
+
+// cpp:52-57: (iu8)(v*255) = cvttsd2si to int32, keep the low byte (A.5)
+__device__ __forceinline__ iu8 nr_to_u8(f64 v) {
+    f64 t = v * 255;
+    if (!(t > -2147483649.0 && t < 2147483648.0)) return 0;
+    return (iu8)((int)t & 0xFF);
+}

@@ -1,0 +1,391 @@
+"""Drop-in mirror of the reference's ctypes module
+(/root/reference/src/libNativeCPURendererPybind.py) for the raster path,
+backed by the HIP library libNativeCPURenderer.so built for gfx950.
+
+Same class names, method names, arities and argument meaning as the
+reference (RenderContext :51-300, Texture :369-435, PtrCreatedTexture
+:437-440, Helpers :11-49, get_version :661-666), so
+``import libnativecpurenderer_amd.libNativeCPURendererPybind as CPURenderer``
+replaces ``import libNativeCPURendererPybind as CPURenderer``
+(milrenderer.py:17) for every raster call.  Additions (triangles, depth,
+numpy readback, timing) are new methods; nothing existing changes meaning.
+
+Deliberate differences from the reference binding, each a reference bug:
+  * get_color passes f64 coordinates (the reference declares c_long for the
+    f64 parameters of GetColor, h:113, and crashes — SURVEY §8b);
+  * Texture(..., is_uint8=False) works (the reference's
+    `c_double * len(data) // 8` precedence bug raises TypeError, :391);
+  * apply_pixel works (the reference .so does not export ApplyPixel).
+Out of scope here (media back-ends): VideoCap, AudioClip,
+the milthm hit-effect shader and WapperedBytes helpers.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import typing
+
+import numpy as np
+
+from . import _lib
+
+lib = _lib.load()
+
+
+def _check(ptr, what: str):
+    if not ptr:
+        raise RuntimeError(f"{what} failed: {_lib.last_error() or 'no HIP device / allocation failure'}")
+    return ptr
+
+
+def _f64_ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Helpers:
+    @staticmethod
+    def get_wappered_bytes_data_ptr(bytes: int):
+        raise NotImplementedError("WapperedBytes belong to the audio back-end (out of scope)")
+
+    @staticmethod
+    def get_wappered_bytes_data_size(bytes: int):
+        raise NotImplementedError("WapperedBytes belong to the audio back-end (out of scope)")
+
+    @staticmethod
+    def wappered_bytes_to_python(bytes: int):
+        raise NotImplementedError("WapperedBytes belong to the audio back-end (out of scope)")
+
+    @staticmethod
+    def create_milthm_hit_effect_textures(mask: "Texture", n: int):
+        raise NotImplementedError("the procedural hit-effect shader is out of scope (SURVEY §8f-3)")
+
+
+class RenderContext:
+    """Framebuffer in HBM + host-side transform/colour state (cpp:3-45)."""
+
+    def __init__(self, width: int, height: int, enable_alpha: bool):
+        self.width = width
+        self.height = height
+        self.enable_alpha = enable_alpha
+        self._can_release = False
+        self._ptr = _check(lib.CreateRenderContext(width, height, enable_alpha), "CreateRenderContext")
+        self._can_release = True
+
+    def __del__(self):
+        if not getattr(self, "_can_release", False):
+            return
+        lib.DestroyRenderContext(self._ptr)
+        self._ptr = 0
+        self._can_release = False
+
+    # ---- readback -------------------------------------------------------
+    def get_buffer_size(self):
+        return lib.GetBufferSize(self._ptr)
+
+    def get_buffer(self):
+        return self.get_buffer_numpy().tolist()
+
+    def get_buffer_as_uint8(self):
+        buffer = bytearray(self.get_buffer_size())
+        lib.GetBufferAsUInt8(self._ptr, (ctypes.c_byte * len(buffer)).from_buffer(buffer))
+        return buffer
+
+    # ---- pixel ops -----------------------------------------------------
+    def fill_color(self, r: float, g: float, b: float, a: float):
+        lib.FillColor(self._ptr, r, g, b, a)
+
+    def draw_texture(self, tex: "Texture", x: float, y: float, w: float, h: float):
+        lib.DrawTexture(self._ptr, tex._ptr, x, y, w, h)
+
+    def resize(self, width: int, height: int):
+        lib.ResizeRenderContext(self._ptr, width, height)
+        self.width = width
+        self.height = height
+
+    def draw_splitted_texture(self, tex: "Texture", x: float, y: float, width: float, height: float,
+                              u_start: float, u_end: float, v_start: float, v_end: float):
+        lib.DrawSplittedTexture(self._ptr, tex._ptr, x, y, width, height, u_start, u_end, v_start, v_end)
+
+    # ---- transform state -----------------------------------------------
+    def apply_transform(self, a: float, b: float, c: float, d: float, e: float, f: float):
+        lib.ApplyTransform(self._ptr, a, b, c, d, e, f)
+
+    def scale(self, sx: float, sy: float):
+        lib.Scale(self._ptr, sx, sy)
+
+    def rotate(self, angle: float):
+        lib.Rotate(self._ptr, angle)
+
+    def translate(self, tx: float, ty: float):
+        lib.Translate(self._ptr, tx, ty)
+
+    def rotate_degree(self, deg: float):
+        self.rotate(deg * math.pi / 180)
+
+    def save_state(self):
+        lib.SaveContextState(self._ptr)
+
+    def restore_state(self):
+        lib.RestoreContextState(self._ptr)
+
+    def draw_line(self, x0: float, y0: float, x1: float, y1: float, width: float,
+                  r: float, g: float, b: float, a: float):
+        lib.DrawLine(self._ptr, x0, y0, x1, y1, width, r, g, b, a)
+
+    def draw_rect(self, x: float, y: float, width: float, height: float, r: float, g: float, b: float, a: float):
+        lib.DrawRect(self._ptr, x, y, width, height, r, g, b, a)
+
+    def get_transform(self):
+        out = (ctypes.c_double * 6)()
+        lib.GetTransform(self._ptr, ctypes.byref(out))
+        return tuple(out)
+
+    def get_inverse_transform(self):
+        out = (ctypes.c_double * 6)()
+        lib.GetInverseTransform(self._ptr, ctypes.byref(out))
+        return tuple(out)
+
+    def apply_pixel(self, x: int, y: int, r: float, g: float, b: float, a: float):
+        lib.ApplyPixel(self._ptr, x, y, r, g, b, a)
+
+    def draw_circle(self, x: float, y: float, radius: float, r: float, g: float, b: float, a: float):
+        lib.DrawCircle(self._ptr, x, y, radius, r, g, b, a)
+
+    def set_transform(self, a: float, b: float, c: float, d: float, e: float, f: float):
+        lib.SetTransform(self._ptr, a, b, c, d, e, f)
+
+    def set_color_transform(self, r: float, g: float, b: float, a: float):
+        lib.SetColorTransform(self._ptr, r, g, b, a)
+
+    def apply_color_transform(self, r: float, g: float, b: float, a: float):
+        lib.ApplyColorTransform(self._ptr, r, g, b, a)
+
+    def set_pixel(self, x: int, y: int, r: float, g: float, b: float, a: float):
+        lib.SetPixel(self._ptr, x, y, r, g, b, a)
+
+    def set_color(self, r: float, g: float, b: float, a: float):
+        lib.SetColor(self._ptr, r, g, b, a)
+
+    def get_color(self, x: float, y: float):
+        out = (ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double())
+        lib.GetColor(self._ptr, x, y, *(ctypes.byref(o) for o in out))
+        return tuple(o.value for o in out)
+
+    def draw_vertical_grd(self, x: float, y: float, width: float, height: float,
+                          top_r: float, top_g: float, top_b: float, top_a: float,
+                          bottom_r: float, bottom_g: float, bottom_b: float, bottom_a: float):
+        lib.DrawVerticalGrd(self._ptr, x, y, width, height, top_r, top_g, top_b, top_a,
+                            bottom_r, bottom_g, bottom_b, bottom_a)
+
+    def draw_vertical_mut_grd(self, x: float, y: float, width: float, height: float,
+                              steps: list[tuple[float, tuple[float, float, float, float]]]):
+        # Pybind.py:272-280: consecutive stops become DrawVerticalGrd bands
+        for i, (p, s) in enumerate(steps):
+            if i == len(steps) - 1:
+                break
+            np_, ns = steps[i + 1]
+            ty = y + height * p
+            theight = height * (np_ - p)
+            self.draw_vertical_grd(x, ty, width, theight, s[0], s[1], s[2], s[3], ns[0], ns[1], ns[2], ns[3])
+
+    def as_texure(self):   # sic: the reference's method name (Pybind.py:282)
+        return PtrCreatedTexture(_check(lib.CreateTextureFromRenderContext(self._ptr), "CreateTextureFromRenderContext"))
+
+    def as_texture_shared(self):
+        res = PtrCreatedTexture(
+            _check(lib.CreateTextureFromRenderContextShared(self._ptr), "CreateTextureFromRenderContextShared"))
+        res._can_release = False
+        return res
+
+    def as_pilimg(self):
+        from PIL import Image
+        return Image.frombytes("RGBA" if self.enable_alpha else "RGB", (self.width, self.height),
+                               bytes(self.get_buffer_as_uint8()))
+
+    # ---- additions: numpy readback -------------------------------------
+    def get_buffer_numpy(self) -> np.ndarray:
+        """Framebuffer as a (H, W, ipp) float64 array (one D2H copy)."""
+        ipp = 4 if self.enable_alpha else 3
+        out = np.empty((self.height, self.width, ipp), dtype=np.float64)
+        lib.GetBuffer(self._ptr, _f64_ptr(out))
+        return out
+
+    def get_buffer_as_uint8_numpy(self) -> np.ndarray:
+        ipp = 4 if self.enable_alpha else 3
+        out = np.empty((self.height, self.width, ipp), dtype=np.uint8)
+        lib.GetBufferAsUInt8(self._ptr, out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+    # ---- additions: triangles + depth ----------------------------------
+    def set_depth_state(self, test: bool, write: bool = True):
+        lib.SetDepthState(self._ptr, bool(test), bool(write))
+
+    def clear_depth(self, value: int = 0xFFFFFFFF):
+        lib.ClearDepth(self._ptr, value)
+
+    def get_depth_buffer(self) -> np.ndarray:
+        out = np.empty((self.height, self.width), dtype=np.uint32)
+        lib.GetDepthBuffer(self._ptr, out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+    def draw_triangles(self, xy, rgba, z=None, gouraud: typing.Optional[bool] = None):
+        """Draws n triangles in the current transform.
+
+        xy: (n, 3, 2) or (n, 6) vertex positions; rgba: (n, 4) flat colours or
+        (n, 3, 4) / (n, 12) per-vertex colours (Gouraud); z: (n, 3) depths in
+        [0, 1] or None."""
+        xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 6)
+        n = xy.shape[0]
+        rgba = np.ascontiguousarray(rgba, dtype=np.float64).reshape(n, -1)
+        if gouraud is None:
+            gouraud = rgba.shape[1] == 12
+        if rgba.shape[1] != (12 if gouraud else 4):
+            raise ValueError("rgba must hold 4 (flat) or 12 (Gouraud) values per triangle")
+        zp = None
+        if z is not None:
+            z = np.ascontiguousarray(z, dtype=np.float64).reshape(n, 3)
+            zp = _f64_ptr(z)
+        lib.DrawTriangles(self._ptr, _f64_ptr(xy), zp, _f64_ptr(rgba), n, bool(gouraud))
+
+    def draw_triangle_buffer(self, buf: "TriangleBuffer"):
+        lib.DrawTriangleBuffer(self._ptr, buf._ptr)
+
+    # ---- additions: sync, device interop, measurement ------------------
+    def flush(self):
+        lib.Flush(self._ptr)
+
+    @property
+    def device(self) -> int:
+        return lib.GetContextDevice(self._ptr)
+
+    def device_buffer_ptr(self) -> int:
+        return lib.GetDeviceBufferPtr(self._ptr)
+
+    def stream_ptr(self) -> int:
+        return lib.GetStreamPtr(self._ptr)
+
+    def enable_kernel_timing(self, on: bool = True):
+        lib.EnableKernelTiming(self._ptr, on)
+
+    def reset_kernel_timing(self):
+        lib.ResetKernelTiming(self._ptr)
+
+    def get_kernel_timing(self, name: str):
+        """(total_ms, launches) of one kernel since the last reset."""
+        tot = ctypes.c_double()
+        cnt = ctypes.c_long()
+        if not lib.GetKernelTiming(self._ptr, name.encode(), ctypes.byref(tot), ctypes.byref(cnt)):
+            raise KeyError(name)
+        return tot.value, cnt.value
+
+    def set_fragment_counting(self, on: bool = True):
+        lib.SetFragmentCounting(self._ptr, on)
+
+    def get_fragment_count(self) -> int:
+        return lib.GetFragmentCount(self._ptr)
+
+
+class Texture:
+    """Texels in HBM as f64, same interleaved layout as the framebuffer
+    (cpp:318-354)."""
+
+    def __init__(self, width: int, height: int, enableAlpha: bool, data: typing.ByteString,
+                 is_uint8: bool = True):
+        if width * height * (3 if not enableAlpha else 4) * (1 if is_uint8 else 8) != len(data):
+            raise ValueError("data size not match")
+        self.width = width
+        self.height = height
+        self.enableAlpha = enableAlpha
+        self._can_release = False
+        data = bytearray(data)
+        if is_uint8:
+            ptr = lib.CreateTextureUInt8(width, height, enableAlpha, (ctypes.c_byte * len(data)).from_buffer(data))
+        else:
+            ptr = lib.CreateTexture(width, height, enableAlpha, (ctypes.c_double * (len(data) // 8)).from_buffer(data))
+        self._ptr = _check(ptr, "CreateTexture")
+        self._can_release = True
+
+    def __del__(self):
+        if not getattr(self, "_can_release", False):
+            return
+        lib.DestroyTexture(self._ptr)
+        self._can_release = False
+
+    def _update_props(self):
+        self.width = lib.GetTextureWidth(self._ptr)
+        self.height = lib.GetTextureHeight(self._ptr)
+        self.enableAlpha = lib.GetTextureEnableAlpha(self._ptr)
+
+    def resample(self, width: int, height: int):
+        return PtrCreatedTexture(_check(lib.ResampleTexture(self._ptr, width, height), "ResampleTexture"))
+
+    def get_buffer_numpy(self) -> np.ndarray:
+        ipp = 4 if self.enableAlpha else 3
+        out = np.empty((self.height, self.width, ipp), dtype=np.float64)
+        lib.GetTextureBuffer(self._ptr, _f64_ptr(out))
+        return out
+
+    @staticmethod
+    def from_pilimg(img):
+        from PIL import Image
+        if not isinstance(img, Image.Image):
+            raise TypeError("img must be a PIL.Image.Image")
+        if img.mode not in ("RGB", "RGBA"):
+            img = img.convert("RGBA")
+        return Texture(img.width, img.height, img.mode == "RGBA", img.tobytes())
+
+    @staticmethod
+    def from_numpy(arr: np.ndarray) -> "Texture":
+        """(H, W, 3|4) uint8 or float64 array -> Texture."""
+        arr = np.ascontiguousarray(arr)
+        h, w, c = arr.shape
+        if arr.dtype == np.uint8:
+            return Texture(w, h, c == 4, arr.tobytes())
+        return Texture(w, h, c == 4, arr.astype(np.float64).tobytes(), is_uint8=False)
+
+
+class PtrCreatedTexture(Texture):
+    def __init__(self, ptr: int):
+        self._ptr = ptr
+        self._can_release = True
+        self._update_props()
+
+
+class TriangleBuffer:
+    """Device-resident triangle soup (new): uploaded once, drawn per frame."""
+
+    def __init__(self, xy, rgba, z=None, gouraud: typing.Optional[bool] = None):
+        xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 6)
+        n = xy.shape[0]
+        rgba = np.ascontiguousarray(rgba, dtype=np.float64).reshape(n, -1)
+        if gouraud is None:
+            gouraud = rgba.shape[1] == 12
+        if rgba.shape[1] != (12 if gouraud else 4):
+            raise ValueError("rgba must hold 4 (flat) or 12 (Gouraud) values per triangle")
+        zp = None
+        if z is not None:
+            z = np.ascontiguousarray(z, dtype=np.float64).reshape(n, 3)
+            zp = _f64_ptr(z)
+        self.n = n
+        self.gouraud = bool(gouraud)
+        self._can_release = False
+        self._ptr = _check(lib.CreateTriangleBuffer(n, _f64_ptr(xy), zp, _f64_ptr(rgba), bool(gouraud)),
+                           "CreateTriangleBuffer")
+        self._can_release = True
+
+    def __del__(self):
+        if getattr(self, "_can_release", False):
+            lib.DestroyTriangleBuffer(self._ptr)
+            self._can_release = False
+
+
+def get_version():
+    return lib.GetVersion()
+
+
+def device_count() -> int:
+    return lib.GetDeviceCount()
+
+
+def set_device(device: int) -> bool:
+    return lib.SetDevice(device)

@@ -1,0 +1,147 @@
+"""GPU parity: the HIP library (through its Pybind mirror) against the CPU
+oracle on the same seeded inputs, bit for bit (f64 framebuffer, u8 readback,
+u32 depth), at fixture sizes and at BASELINE.json's full sizes."""
+import os
+
+import numpy as np
+import pytest
+
+import scenes
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def assert_same(a: dict, b: dict, what=""):
+    assert set(a) == set(b), (what, set(a) ^ set(b))
+    for k in a:
+        assert scenes.bits_equal(a[k], b[k]), f"{what}/{k}: {scenes.first_mismatch(a[k], b[k])}"
+
+
+@pytest.mark.parametrize("name", sorted(scenes.all_scenes()))
+def test_scene_parity(gpu, oracle, golden, name):
+    g = scenes.run_scene(name, gpu)
+    o = scenes.run_scene(name, oracle)
+    assert_same(g, o, name)
+    for k, v in g.items():
+        assert scenes.bits_equal(v, golden[f"{name}/{k}"]), f"{name}/{k} vs golden"
+
+
+def _c1(fac, rotated):
+    img = np.load(os.path.join(GOLDEN, "image_png_rgba.npy"))
+    ctx = fac.context(256, 256, True)
+    ctx.set_color(0, 0, 0, 0)
+    tex = fac.texture(img)
+    if rotated:
+        ctx.translate(128, 128)
+        ctx.rotate(0.3)
+        ctx.translate(-128, -128)
+    ctx.draw_texture(tex, 64, 64, 128, 128)
+    return {"f64": ctx.get_buffer_numpy(), "u8": ctx.get_buffer_as_uint8_numpy()}
+
+
+@pytest.mark.parametrize("rotated", [False, True])
+def test_c1_textured_quad(gpu, oracle, rotated):
+    assert_same(_c1(gpu, rotated), _c1(oracle, rotated), f"C1 rotated={rotated}")
+
+
+def _tri_frame(fac, W, H, xy, z, c, depth=True, write=True, alpha=False, clear=0.0):
+    ctx = fac.context(W, H, alpha)
+    ctx.set_color(clear, clear, clear, clear)
+    ctx.set_depth_state(depth, write)
+    ctx.clear_depth()
+    ctx.draw_triangles(xy, c, z=z)
+    out = {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}
+    return out, ctx
+
+
+def test_c2_flat_depth_1080p(gpu, oracle):
+    xy, z, c = scenes.triangle_soup(10000, 1920, 1080, 32, seed=1234)
+    g, gctx = _tri_frame(gpu, 1920, 1080, xy, z, c)
+    o, octx = _tri_frame(oracle, 1920, 1080, xy, z, c)
+    assert_same(g, o, "C2")
+
+
+def test_c3_gouraud_depth_4k(gpu, oracle):
+    xy, z, c = scenes.sphere_mesh(3840, 2160, 500, 1000)
+    g, _ = _tri_frame(gpu, 3840, 2160, xy, z, c)
+    o, _ = _tri_frame(oracle, 3840, 2160, xy, z, c)
+    assert_same(g, o, "C3")
+
+
+def test_c5_blend_overdraw_reduced(gpu, oracle):
+    # C5 shape (back-to-front, a in [0.2, 0.8], Z test on, write off) at 1/10
+    # of the triangle count so the oracle finishes in seconds.
+    xy, z, c = scenes.triangle_soup(5000, 1920, 1080, 256, seed=1234, alpha=(0.2, 0.8))
+    order = np.argsort(-z.mean(axis=1), kind="stable")
+    xy, z, c = xy[order], z[order], c[order]
+    g, _ = _tri_frame(gpu, 1920, 1080, xy, z, c, write=False)
+    o, _ = _tri_frame(oracle, 1920, 1080, xy, z, c, write=False)
+    assert_same(g, o, "C5/10")
+
+
+def test_fragment_counter_matches_oracle(gpu, oracle):
+    xy, z, c = scenes.triangle_soup(3000, 640, 480, 20, seed=8, gouraud=True)
+    ctx = gpu.context(640, 480, False)
+    ctx.set_color(0, 0, 0, 0)
+    ctx.set_fragment_counting(True)
+    ctx.draw_triangles(xy, c, z=z)
+    octx = oracle.context(640, 480, False)
+    octx.set_color(0, 0, 0, 0)
+    octx.draw_triangles(xy, c, z=z)
+    assert ctx.get_fragment_count() == octx.last_fragment_count() > 0
+
+
+def test_triangle_buffer_equals_host_arrays(gpu):
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    xy, z, c = scenes.triangle_soup(5000, 500, 300, 15, seed=9, gouraud=True)
+    a, _ = _tri_frame(gpu, 500, 300, xy, z, c)
+    ctx = gpu.context(500, 300, False)
+    ctx.set_color(0, 0, 0, 0)
+    ctx.set_depth_state(True, True)
+    ctx.clear_depth()
+    buf = R.TriangleBuffer(xy, c, z=z)
+    ctx.draw_triangle_buffer(buf)
+    assert_same(a, {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, "buffer")
+
+
+def test_c3_order_independent_depth_full_size(gpu):
+    """Size-independent property at full C3 size: with LESS + write the depth
+    buffer is min(clear, min zq) whatever the submission order."""
+    xy, z, c = scenes.sphere_mesh(3840, 2160, 500, 1000)
+    perm = scenes.rng(3).permutation(len(xy))
+    a, _ = _tri_frame(gpu, 3840, 2160, xy, z, c)
+    b, _ = _tri_frame(gpu, 3840, 2160, xy[perm], z[perm], c[perm])
+    assert np.array_equal(a["depth"], b["depth"])
+    assert (a["depth"] != 0xFFFFFFFF).sum() > 3_000_000
+
+
+def test_repeat_frames_are_deterministic(gpu):
+    xy, z, c = scenes.triangle_soup(20000, 1280, 720, 40, seed=10, alpha=(0.3, 1.0))
+    outs = [_tri_frame(gpu, 1280, 720, xy, z, c, write=False)[0] for _ in range(2)]
+    assert_same(outs[0], outs[1], "repeat")
+
+
+def test_empty_and_offscreen_batches(gpu, oracle):
+    xy = np.array([[-50, -50, -40, -45, -45, -30], [5000, 10, 5100, 20, 5050, 40]], np.float64)
+    c = np.ones((2, 4))
+    for n in (0, 2):
+        g, _ = _tri_frame(gpu, 64, 64, xy[:n], None, c[:n], clear=0.5)
+        o, _ = _tri_frame(oracle, 64, 64, xy[:n], None, c[:n], clear=0.5)
+        assert_same(g, o, f"empty n={n}")
+
+
+def test_resize_and_reuse(gpu, oracle):
+    outs = []
+    for fac in (gpu, oracle):
+        ctx = fac.context(50, 40, False)
+        ctx.set_color(0, 0, 0, 0)
+        ctx.draw_rect(3, 3, 20, 20, 1, 0, 0, 1)
+        ctx.resize(70, 33)
+        ctx.set_color(0.3, 0.3, 0.3, 0.3)
+        xy, z, c = scenes.triangle_soup(300, 70, 33, 8, seed=12)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.draw_triangles(xy, c, z=z)
+        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+    assert_same(outs[0], outs[1], "resize")
