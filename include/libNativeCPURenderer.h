@@ -102,6 +102,8 @@ void DrawTriangleBuffer(RenderContext* ctx, TriangleBuffer* tb);         /* NEW 
 i64 GetTriangleBufferCount(TriangleBuffer* tb);                          /* NEW */
 void SetFragmentCounting(RenderContext* ctx, bool on);                   /* NEW: covered-fragment counter */
 i64 GetFragmentCount(RenderContext* ctx);                                /* NEW */
+i64 GetLastRasterPath(RenderContext* ctx);                               /* NEW: 1 order-free, 2 ordered */
+void SetForceOrderedRaster(RenderContext* ctx, bool on);                 /* NEW: A/B and tests */
 
 /* ---- NEW: device, sync, interop, errors, measurement --------------------- */
 bool SetDevice(i64 device);                      /* device for objects created next on this thread */

@@ -76,6 +76,8 @@ DEVICE_ABI = {
     "GetTriangleBufferCount": (L, (P,)),
     "SetFragmentCounting": (None, (P, B)),
     "GetFragmentCount": (L, (P,)),
+    "GetLastRasterPath": (L, (P,)),
+    "SetForceOrderedRaster": (None, (P, B)),
     "GetLastErrorString": (ctypes.c_char_p, ()),
     "ClearLastError": (None, ()),
     "SetDevice": (B, (L,)),

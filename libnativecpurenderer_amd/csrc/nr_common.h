@@ -42,6 +42,7 @@ struct TriScratch {
     void* temp = nullptr; size_t temp_bytes = 0;                        // hipcub scratch
     u64* h_total = nullptr;                 // pinned readback: [0] pairs, [1] last count, [2] fragments
     u64* d_frag = nullptr;                  // device fragment counter
+    u32* d_flag = nullptr;                  // device non-opaque flag
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
 };
 
@@ -76,6 +77,8 @@ struct RenderContext {
     bool countFragments = false;
     bool fragPending = false;
     u64 fragTotal = 0;
+    int lastPath = 0;                 // raster of the last triangle batch (1 order-free, 2 ordered)
+    int forceOrdered = 0;             // testing: always take the ordered raster
 };
 
 struct Texture {
@@ -93,6 +96,7 @@ struct TriangleBuffer {
     f64* xy = nullptr;    // n*6   (x0,y0,x1,y1,x2,y2)
     f64* z = nullptr;     // n*3 or null
     f64* rgba = nullptr;  // n*4 (flat) or n*12 (Gouraud)
+    bool opaque = false;  // every vertex alpha == 1 (known at upload)
     int device = 0;
 };
 

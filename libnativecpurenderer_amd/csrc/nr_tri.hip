@@ -99,15 +99,33 @@ __device__ __forceinline__ bool tri_tiles(const f64 (&sx)[3], const f64 (&sy)[3]
     return true;
 }
 
-__global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt) {
+// Per-triangle tile count.  With `nonopaque` set, also flags any vertex
+// alpha != 1 (device-pointer batches whose opacity the host cannot know).
+__global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt,
+                                                   u32* __restrict__ nonopaque) {
     const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
-    if (t >= bp.src.n) return;
-    f64 sx[3], sy[3];
-    tri_screen(bp.src, bp.m, t, sx, sy);
-    int tx0, tx1, ty0, ty1;
-    unsigned long long c = 0;
-    if (tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) c = (unsigned long long)(tx1 - tx0 + 1) * (ty1 - ty0 + 1);
-    cnt[t] = c;
+    bool bad = false;
+    if (t < bp.src.n) {
+        f64 sx[3], sy[3];
+        tri_screen(bp.src, bp.m, t, sx, sy);
+        int tx0, tx1, ty0, ty1;
+        unsigned long long c = 0;
+        if (tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1))
+            c = (unsigned long long)(tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+        cnt[t] = c;
+        if (nonopaque) {
+            if (bp.src.gouraud) {
+                const f64* a = bp.src.rgba + t * 12;
+                bad = a[3] != 1 || a[7] != 1 || a[11] != 1;
+            } else {
+                bad = bp.src.rgba[t * 4 + 3] != 1;
+            }
+        }
+    }
+    if (nonopaque) {
+        const unsigned long long m = __ballot(bad);
+        if (m && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1)) atomicOr(nonopaque, 1u);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_tri_emit(const BinParams bp, const unsigned long long* __restrict__ off,
@@ -353,6 +371,237 @@ __global__ __launch_bounds__(WG) void k_tile_raster(const RasterParams rp) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Order-free raster for opaque batches (every fragment overwrites: alpha == 1
+// after the colour transform).  Sequential semantics then reduce per pixel to
+//   Z LESS + write : winner = min over (zq, tri) with zq < z_init -> key min
+//   Z LESS, no write: winner = last tri with zq < z_init           -> id max
+//   no Z test       : winner = last covering tri                    -> id max
+// so fragments are processed in any order with 64-bit LDS atomics on a packed
+// key ((zq << 32) | tri+1), then one resolve per pixel shades only the winner
+// (deferred shading).  Bit-identical to the ordered path by construction.
+// Fragment-parallel: per 256-triangle chunk the exact row spans are counted,
+// prefix-summed, and every thread takes fragments (binary search -> tri, row
+// walk -> x), so tiny triangles keep all 64 lanes busy.
+// ---------------------------------------------------------------------------
+constexpr int FCH = 256;
+enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_E1X, F_E1Y, F_E2X, F_E2Y, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
+
+template <int ZMODE, bool GOURAUD, bool COUNT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+__global__ __launch_bounds__(WG) void k_tile_raster_free(const RasterParams rp) {
+    constexpr bool DEPTH = ZMODE != 0;
+    const int tile = blockIdx.x;
+    const int tx = tile % rp.tiles_x, ty = tile / rp.tiles_x;
+    const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
+    const int tid = threadIdx.x;
+    const u32 ls = rp.tstart[tile], le = rp.tend[tile];
+    if (ls == le && !rp.pendColor && !(DEPTH && rp.pendDepth)) return;
+
+    __shared__ u64 key[TH * TW];
+    __shared__ u32 zin[ZMODE == 2 ? TH * TW : 1];
+    __shared__ f64 S[F_NSLOT][FCH];
+    __shared__ u32 TIDX[FCH];
+    __shared__ iu8 XS[FCH][TH], XE[FCH][TH];
+    __shared__ u32 OFF[FCH + 1];
+    __shared__ iu8 RR0[FCH];
+
+    const int wlim = (int)(rp.W - x0 < TW ? rp.W - x0 : TW);
+    const int hlim = (int)(rp.H - y0 < TH ? rp.H - y0 : TH);
+    for (int p = tid; p < TH * TW; p += WG) {
+        const int lx = p & (TW - 1), ly = p / TW;
+        u32 z0 = 0xFFFFFFFFu;
+        if (DEPTH && lx < wlim && ly < hlim)
+            z0 = rp.pendDepth ? rp.pendDepthValue : rp.depth[(y0 + ly) * rp.W + x0 + lx];
+        key[p] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
+        if (ZMODE == 2) zin[p] = z0;
+    }
+    u64 fragTotal = 0;
+
+    for (u32 base = ls; base < le; base += FCH) {
+        const int cnt = (le - base) < (u32)FCH ? (int)(le - base) : FCH;
+        __syncthreads();
+        // ---- (a) setup + exact spans, one thread per triangle
+        if (tid < cnt) {
+            const u32 t = rp.list[base + tid];
+            f64 sx[3], sy[3];
+            tri_screen(rp.src, rp.m, t, sx, sy);
+            bool ok = isfinite(sx[0]) && isfinite(sy[0]) && isfinite(sx[1]) && isfinite(sy[1]) &&
+                      isfinite(sx[2]) && isfinite(sy[2]);
+            const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+            const f64 den = e1x * e2y - e2x * e1y;
+            ok = ok && den != 0;
+            S[F_X0][tid] = sx[0]; S[F_Y0][tid] = sy[0];
+            S[F_E1X][tid] = e1x; S[F_E1Y][tid] = e1y; S[F_E2X][tid] = e2x; S[F_E2Y][tid] = e2y;
+            S[F_INV][tid] = 1.0 / den;
+            if (DEPTH) {
+                f64 z0 = 0, z1 = 0, z2 = 0;
+                if (rp.src.z) { z0 = rp.src.z[(i64)t * 3]; z1 = rp.src.z[(i64)t * 3 + 1]; z2 = rp.src.z[(i64)t * 3 + 2]; }
+                S[F_Z0][tid] = z0; S[F_DZ1][tid] = z1 - z0; S[F_DZ2][tid] = z2 - z0;
+            }
+            TIDX[tid] = t;
+            int r0 = 0;
+            u32 nf = 0;
+            if (ok) {
+                // rows with a straddling edge: ymin <= y < ymax (exact)
+                const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+                r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
+                const int r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
+                for (int r = r0; r < r1; ++r) {
+                    const f64 y = (f64)(y0 + r);
+                    f64 c[2] = {0, 0};
+                    int nc = 0;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const int j = (i + 2) % 3;
+                        if ((sy[i] > y) != (sy[j] > y)) {
+                            const f64 cc = (sx[j] - sx[i]) * (y - sy[i]) / (sy[j] - sy[i]) + sx[i];
+                            if (nc == 0) c[0] = cc; else c[1] = cc;
+                            ++nc;
+                        }
+                    }
+                    int xs = 0, xe = 0;
+                    if (nc == 2) {
+                        const f64 lo = fmin(c[0], c[1]), hi = fmax(c[0], c[1]);
+                        xs = (int)clampd(ceil(lo) - (f64)x0, 0.0, (f64)wlim);
+                        xe = (int)clampd(ceil(hi) - (f64)x0, 0.0, (f64)wlim);
+                        if (xe < xs) xe = xs;
+                    }
+                    XS[tid][r] = (iu8)xs;
+                    XE[tid][r] = (iu8)xe;
+                    nf += (u32)(xe - xs);
+                }
+            }
+            RR0[tid] = (iu8)r0;
+            OFF[tid] = nf;
+        }
+        __syncthreads();
+        // ---- (b) exclusive scan of the fragment counts (wave 0)
+        if (tid < 64) {
+            u32 v[FCH / 64];
+            u32 sum = 0;
+#pragma unroll
+            for (int i = 0; i < FCH / 64; ++i) {
+                const int idx = tid * (FCH / 64) + i;
+                v[i] = idx < cnt ? OFF[idx] : 0u;
+                sum += v[i];
+            }
+            u32 incl = sum;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const u32 o = __shfl_up(incl, d, 64);
+                if (tid >= d) incl += o;
+            }
+            u32 ex = incl - sum;
+#pragma unroll
+            for (int i = 0; i < FCH / 64; ++i) {
+                OFF[tid * (FCH / 64) + i] = ex;
+                ex += v[i];
+            }
+            if (tid == 63) OFF[FCH] = incl;
+        }
+        __syncthreads();
+        // ---- (c) fragment-parallel visibility
+        const u32 F = OFF[cnt];
+        if (COUNT) fragTotal += F;
+        for (u32 f = tid; f < F; f += WG) {
+            int lo = 0, hi = cnt;            // OFF[lo] <= f < OFF[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (OFF[mid] <= f) lo = mid; else hi = mid;
+            }
+            const int k = lo;
+            u32 l = f - OFF[k];
+            int r = RR0[k];
+            for (;;) {
+                const u32 len = (u32)(XE[k][r] - XS[k][r]);
+                if (l < len) break;
+                l -= len;
+                ++r;
+            }
+            const int lx = XS[k][r] + (int)l;
+            const int p = r * TW + lx;
+            const u64 id1 = (u64)TIDX[k] + 1;
+            if (ZMODE == 0) {
+                atomicMax(&key[p], id1);
+            } else {
+                const f64 dx = (f64)(x0 + lx) - S[F_X0][k], dy = (f64)(y0 + r) - S[F_Y0][k];
+                const f64 w1 = (dx * S[F_E2Y][k] - S[F_E2X][k] * dy) * S[F_INV][k];
+                const f64 w2 = (S[F_E1X][k] * dy - dx * S[F_E1Y][k]) * S[F_INV][k];
+                const f64 zz = S[F_Z0][k] + S[F_DZ1][k] * w1 + S[F_DZ2][k] * w2;
+                const u32 zq = nr_quantize_depth(zz);
+                if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
+                else if (zq < zin[p]) atomicMax(&key[p], id1);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- resolve: one pass over the tile, shading only the winners
+    const int ipp = rp.ipp;
+    const f64 ct0 = rp.ct[0], ct1 = rp.ct[1], ct2 = rp.ct[2], ct3 = rp.ct[3];
+    for (int p = tid; p < TH * TW; p += WG) {
+        const int lx = p & (TW - 1), ly = p / TW;
+        if (lx >= wlim || ly >= hlim) continue;
+        const i64 px = x0 + lx, py = y0 + ly;
+        f64* dst = rp.fb + (py * rp.W + px) * ipp;
+        f64 R, G, B, A = 0;
+        if (rp.pendColor) {
+            R = G = B = A = rp.pendColorValue;
+        } else {
+            R = dst[0]; G = dst[1]; B = dst[2];
+            if (ipp == 4) A = dst[3];
+        }
+        const u64 kv = key[p];
+        const u32 id1 = (u32)kv;
+        if (id1) {
+            const i64 t = (i64)id1 - 1;
+            f64 sx[3], sy[3];
+            tri_screen(rp.src, rp.m, t, sx, sy);
+            const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+            const f64 inv = 1.0 / (e1x * e2y - e2x * e1y);
+            f64 cr, cg, cb, ca;
+            if (GOURAUD) {
+                const f64 dx = (f64)px - sx[0], dy = (f64)py - sy[0];
+                const f64 w1 = (dx * e2y - e2x * dy) * inv;
+                const f64 w2 = (e1x * dy - dx * e1y) * inv;
+                const f64* c = rp.src.rgba + t * 12;
+                cr = c[0] + (c[4] - c[0]) * w1 + (c[8] - c[0]) * w2;
+                cg = c[1] + (c[5] - c[1]) * w1 + (c[9] - c[1]) * w2;
+                cb = c[2] + (c[6] - c[2]) * w1 + (c[10] - c[2]) * w2;
+                ca = c[3] + (c[7] - c[3]) * w1 + (c[11] - c[3]) * w2;
+            } else {
+                const f64* c = rp.src.rgba + t * 4;
+                cr = c[0]; cg = c[1]; cb = c[2]; ca = c[3];
+            }
+            // ApplyPixel (cpp:529-547); A == 1 for every batch routed here
+            cr *= ct0; cg *= ct1; cb *= ct2; ca *= ct3;
+            if (ca != 1) {
+                cr = R * (1 - ca) + cr * ca;
+                cg = G * (1 - ca) + cg * ca;
+                cb = B * (1 - ca) + cb * ca;
+            }
+            R = cr; G = cg; B = cb; A = ca;
+        }
+        dst[0] = R; dst[1] = G; dst[2] = B;
+        if (ipp == 4) dst[3] = A;
+        if (ZMODE == 1) rp.depth[py * rp.W + px] = (u32)(kv >> 32);
+        else if (ZMODE == 2 && rp.pendDepth) rp.depth[py * rp.W + px] = zin[p];
+    }
+    if (COUNT && tid == 0) atomicAdd(rp.fragCounter, fragTotal);
+}
+
+template <int Z, bool G, bool C>
+void launch_free(const RasterParams& rp, int ntiles, hipStream_t s) {
+    hipLaunchKernelGGL((k_tile_raster_free<Z, G, C>), dim3(ntiles), dim3(WG), 0, s, rp);
+}
+
+template <bool C>
+void launch_free_c(const RasterParams& rp, int zmode, bool g, int ntiles, hipStream_t s) {
+    if (zmode == 1) { if (g) launch_free<1, true, C>(rp, ntiles, s); else launch_free<1, false, C>(rp, ntiles, s); }
+    else if (zmode == 2) { if (g) launch_free<2, true, C>(rp, ntiles, s); else launch_free<2, false, C>(rp, ntiles, s); }
+    else { if (g) launch_free<0, true, C>(rp, ntiles, s); else launch_free<0, false, C>(rp, ntiles, s); }
+}
+
 template <bool G, bool D, bool C>
 void launch_raster(const RasterParams& rp, int ntiles, hipStream_t s) {
     hipLaunchKernelGGL((k_tile_raster<G, D, C>), dim3(ntiles), dim3(WG), 0, s, rp);
@@ -397,8 +646,20 @@ static bool grow_temp(TriScratch& sc, size_t need) {
     return true;
 }
 
+// Opacity of a batch: every vertex alpha == 1 (then, with colourTransform[3]
+// == 1, every fragment overwrites and the order-free raster applies).
+enum Opacity { OPQ_UNKNOWN = 0, OPQ_OPAQUE, OPQ_BLENDED };
+
+static Opacity host_opacity(const f64* rgba, i64 n, bool gouraud) {
+    const i64 stride = gouraud ? 12 : 4;
+    for (i64 t = 0; t < n; ++t)
+        for (int v = 0; v < (gouraud ? 3 : 1); ++v)
+            if (rgba[t * stride + v * 4 + 3] != 1) return OPQ_BLENDED;
+    return OPQ_OPAQUE;
+}
+
 // Bins + rasterises one batch (all triangles of one draw call).
-static void draw_batch(RenderContext* ctx, const TriSrc& src) {
+static void draw_batch(RenderContext* ctx, const TriSrc& src, Opacity opq) {
     if (src.n <= 0 || ctx->width <= 0 || ctx->height <= 0) return;
     hipStream_t s = ctx->stream;
     TriScratch& sc = ctx->tri;
@@ -420,11 +681,17 @@ static void draw_batch(RenderContext* ctx, const TriSrc& src) {
     if (!grow_set(tile_bufs, &sc.tile_cap, (size_t)ntiles)) return;
     sc.tile_start = tile_bufs[0]; sc.tile_end = tile_bufs[1];
     if (!sc.h_total) NR_CHECK(hipHostMalloc((void**)&sc.h_total, 4 * sizeof(u64)));
+    if (!sc.d_flag) NR_CHECK(hipMalloc(&sc.d_flag, sizeof(u32)));
+    u32* nonopaque = nullptr;
+    if (opq == OPQ_UNKNOWN && ctx->ct[3] == 1) {
+        NR_CHECK(hipMemsetAsync(sc.d_flag, 0, sizeof(u32), s));
+        nonopaque = sc.d_flag;
+    }
 
     const int g1 = (int)((src.n + 255) / 256);
     hipEvent_t e0, e1;
     nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
-    hipLaunchKernelGGL(k_tri_count, dim3(g1), dim3(256), 0, s, bp, sc.cnt);
+    hipLaunchKernelGGL(k_tri_count, dim3(g1), dim3(256), 0, s, bp, sc.cnt, nonopaque);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
 
@@ -438,8 +705,13 @@ static void draw_batch(RenderContext* ctx, const TriSrc& src) {
     // total pair count: the one host sync of the pipeline (sizes the sort)
     NR_CHECK(hipMemcpyAsync(&sc.h_total[0], sc.off + (src.n - 1), sizeof(u64), hipMemcpyDeviceToHost, s));
     NR_CHECK(hipMemcpyAsync(&sc.h_total[1], sc.cnt + (src.n - 1), sizeof(u64), hipMemcpyDeviceToHost, s));
+    if (nonopaque) {
+        sc.h_total[3] = 0;
+        NR_CHECK(hipMemcpyAsync(&sc.h_total[3], nonopaque, sizeof(u32), hipMemcpyDeviceToHost, s));
+    }
     NR_CHECK(hipStreamSynchronize(s));
     const u64 P = sc.h_total[0] + sc.h_total[1];
+    if (nonopaque) opq = (sc.h_total[3] & 0xFFFFFFFFull) ? OPQ_BLENDED : OPQ_OPAQUE;
 
     if (P > (1ull << 31) && src.n > 1) {
         // too many pairs for one pass: split the batch; submission order kept
@@ -449,8 +721,8 @@ static void draw_batch(RenderContext* ctx, const TriSrc& src) {
         b.xy = src.xy + a.n * 6;
         b.z = src.z ? src.z + a.n * 3 : nullptr;
         b.rgba = src.rgba + a.n * (src.gouraud ? 12 : 4);
-        draw_batch(ctx, a);
-        draw_batch(ctx, b);
+        draw_batch(ctx, a, opq);
+        draw_batch(ctx, b, opq);
         return;
     }
 
@@ -512,9 +784,18 @@ static void draw_batch(RenderContext* ctx, const TriSrc& src) {
         rp.fragCounter = sc.d_frag;
     }
 
+    // every fragment overwrites -> order-free visibility + deferred shading
+    const bool orderFree = opq == OPQ_OPAQUE && ctx->ct[3] == 1 && ctx->forceOrdered == 0;
+    const int zmode = depth ? (ctx->depthWrite ? 1 : 2) : 0;
+    ctx->lastPath = orderFree ? 1 : 2;
     nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-    if (rp.fragCounter) launch_raster_c<true>(rp, src.gouraud != 0, depth, ntiles, s);
-    else launch_raster_c<false>(rp, src.gouraud != 0, depth, ntiles, s);
+    if (orderFree) {
+        if (rp.fragCounter) launch_free_c<true>(rp, zmode, src.gouraud != 0, ntiles, s);
+        else launch_free_c<false>(rp, zmode, src.gouraud != 0, ntiles, s);
+    } else {
+        if (rp.fragCounter) launch_raster_c<true>(rp, src.gouraud != 0, depth, ntiles, s);
+        else launch_raster_c<false>(rp, src.gouraud != 0, depth, ntiles, s);
+    }
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
 
@@ -562,7 +843,16 @@ void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const 
     if (n <= 0) return;
     if (!ctx->depthTest) nr_materialize_depth(ctx);
     TriSrc src{xy, z, rgba, gouraud ? 1 : 0, n};
-    draw_batch(ctx, src);
+    draw_batch(ctx, src, OPQ_UNKNOWN);
+}
+
+static void draw_known(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud,
+                       Opacity opq) {
+    NR_CHECK(hipSetDevice(ctx->device));
+    if (n <= 0) return;
+    if (!ctx->depthTest) nr_materialize_depth(ctx);
+    TriSrc src{xy, z, rgba, gouraud ? 1 : 0, n};
+    draw_batch(ctx, src, opq);
 }
 
 // New: triangles from host arrays (copied to HBM first).
@@ -581,7 +871,7 @@ void DrawTriangles(RenderContext* ctx, const f64* xy, const f64* z, const f64* r
     if (z) NR_CHECK(hipMemcpyAsync(dz, z, (size_t)n * 3 * sizeof(f64), hipMemcpyHostToDevice, ctx->stream));
     NR_CHECK(hipMemcpyAsync(dc, rgba, (size_t)n * ncol * sizeof(f64), hipMemcpyHostToDevice, ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));   // caller may reuse its arrays on return
-    DrawTrianglesDevice(ctx, dxy, z ? dz : nullptr, dc, n, gouraud);
+    draw_known(ctx, dxy, z ? dz : nullptr, dc, n, gouraud, host_opacity(rgba, n, gouraud));
 }
 
 // New: a device-resident triangle soup (the H2D point; drawn many times).
@@ -589,6 +879,7 @@ TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f
     TriangleBuffer* tb = new TriangleBuffer();
     tb->n = n;
     tb->gouraud = gouraud;
+    tb->opaque = n > 0 && host_opacity(rgba, n, gouraud) == OPQ_OPAQUE;
     NR_CHECK(hipGetDevice(&tb->device));
     hipStream_t s = nr_stream_for(tb->device);
     const size_t ncol = gouraud ? 12 : 4;
@@ -628,7 +919,13 @@ void SetFragmentCounting(RenderContext* ctx, bool on) {
 i64 GetFragmentCount(RenderContext* ctx) { return (i64)ctx->fragTotal; }
 
 void DrawTriangleBuffer(RenderContext* ctx, TriangleBuffer* tb) {
-    DrawTrianglesDevice(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud);
+    draw_known(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud, tb->opaque ? OPQ_OPAQUE : OPQ_BLENDED);
 }
+
+// New: which raster the last batch took (1 = order-free, 2 = ordered).
+i64 GetLastRasterPath(RenderContext* ctx) { return ctx->lastPath; }
+
+// New (testing / A-B measurement): force the ordered raster for every batch.
+void SetForceOrderedRaster(RenderContext* ctx, bool on) { ctx->forceOrdered = on ? 1 : 0; }
 
 }  // extern "C"

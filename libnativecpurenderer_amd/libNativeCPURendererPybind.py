@@ -236,9 +236,10 @@ class RenderContext:
         [0, 1] or None."""
         xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 6)
         n = xy.shape[0]
-        rgba = np.ascontiguousarray(rgba, dtype=np.float64).reshape(n, -1)
+        rgba = np.ascontiguousarray(rgba, dtype=np.float64)
         if gouraud is None:
-            gouraud = rgba.shape[1] == 12
+            gouraud = rgba.size == 12 * n and n > 0
+        rgba = rgba.reshape(n, 12 if gouraud else 4)
         if rgba.shape[1] != (12 if gouraud else 4):
             raise ValueError("rgba must hold 4 (flat) or 12 (Gouraud) values per triangle")
         zp = None
@@ -283,6 +284,12 @@ class RenderContext:
 
     def get_fragment_count(self) -> int:
         return lib.GetFragmentCount(self._ptr)
+
+    def last_raster_path(self) -> str:
+        return {0: "none", 1: "order-free", 2: "ordered"}[lib.GetLastRasterPath(self._ptr)]
+
+    def set_force_ordered_raster(self, on: bool = True):
+        lib.SetForceOrderedRaster(self._ptr, on)
 
 
 class Texture:
@@ -357,9 +364,10 @@ class TriangleBuffer:
     def __init__(self, xy, rgba, z=None, gouraud: typing.Optional[bool] = None):
         xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 6)
         n = xy.shape[0]
-        rgba = np.ascontiguousarray(rgba, dtype=np.float64).reshape(n, -1)
+        rgba = np.ascontiguousarray(rgba, dtype=np.float64)
         if gouraud is None:
-            gouraud = rgba.shape[1] == 12
+            gouraud = rgba.size == 12 * n and n > 0
+        rgba = rgba.reshape(n, 12 if gouraud else 4)
         if rgba.shape[1] != (12 if gouraud else 4):
             raise ValueError("rgba must hold 4 (flat) or 12 (Gouraud) values per triangle")
         zp = None

@@ -145,3 +145,22 @@ def test_resize_and_reuse(gpu, oracle):
         ctx.draw_triangles(xy, c, z=z)
         outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
     assert_same(outs[0], outs[1], "resize")
+
+
+@pytest.mark.parametrize("mode", ["depth_write", "depth_nowrite", "nodepth"])
+@pytest.mark.parametrize("gouraud", [False, True])
+def test_order_free_equals_ordered(gpu, mode, gouraud):
+    """The order-free raster (opaque batches) and the ordered raster agree bit
+    for bit, and the opaque batch really takes the order-free path."""
+    xy, z, c = scenes.triangle_soup(4000, 700, 500, 25, seed=31, gouraud=gouraud)
+    outs = []
+    for force in (False, True):
+        ctx = gpu.context(700, 500, True)
+        ctx.set_force_ordered_raster(force)
+        ctx.set_color(0.25, 0.25, 0.25, 0.25)
+        ctx.set_depth_state(mode != "nodepth", mode == "depth_write")
+        ctx.clear_depth(0xF0000000)
+        ctx.draw_triangles(xy, c, z=z)
+        assert ctx.last_raster_path() == ("ordered" if force else "order-free")
+        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+    assert_same(outs[0], outs[1], f"free-vs-ordered {mode} g={gouraud}")
