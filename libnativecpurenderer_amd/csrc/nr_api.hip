@@ -290,7 +290,7 @@ void DestroyRenderContext(RenderContext* ctx) {
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
-                    t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag};
+                    t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));
@@ -344,17 +344,26 @@ void GetBuffer(RenderContext* ctx, f64* out) {
     NR_CHECK(hipStreamSynchronize(ctx->stream));
 }
 
-// cpp:52-57: converted on the GPU, 1/8 of the bytes cross PCIe
+// cpp:52-57: converted on the GPU, 1/8 of the bytes cross PCIe.  The u8
+// staging buffer is owned by the context (no stream-ordered allocator).
 void GetBufferAsUInt8(RenderContext* ctx, iu8* out) {
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
     i64 n = GetBufferSize(ctx);
-    iu8* d = nullptr;
-    NR_CHECK(hipMallocAsync((void**)&d, (size_t)(n > 0 ? n : 1), ctx->stream));
-    hipLaunchKernelGGL(k_to_u8, dim3(grid_for(n)), dim3(256), 0, ctx->stream, ctx->buffer, d, n);
+    if (n <= 0) return;
+    if ((size_t)n > ctx->u8cap) {
+        if (ctx->u8buf) NR_CHECK(hipFree(ctx->u8buf));
+        ctx->u8buf = nullptr;
+        if (hipMalloc((void**)&ctx->u8buf, (size_t)n) != hipSuccess) {
+            nr_set_error_msg("GetBufferAsUInt8: hipMalloc failed");
+            ctx->u8cap = 0;
+            return;
+        }
+        ctx->u8cap = (size_t)n;
+    }
+    hipLaunchKernelGGL(k_to_u8, dim3(grid_for(n)), dim3(256), 0, ctx->stream, ctx->buffer, ctx->u8buf, n);
     NR_CHECK(hipGetLastError());
-    NR_CHECK(hipMemcpyAsync(out, d, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
-    NR_CHECK(hipFreeAsync(d, ctx->stream));
+    NR_CHECK(hipMemcpyAsync(out, ctx->u8buf, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));
 }
 
@@ -397,11 +406,12 @@ Texture* CreateTextureUInt8(i64 width, i64 height, bool enableAlpha, iu8* buffer
     i64 size = width * height * (enableAlpha ? 4 : 3);
     if (size > 0) {
         iu8* d = nullptr;
-        NR_CHECK(hipMallocAsync((void**)&d, (size_t)size, s));
+        NR_CHECK(hipMalloc((void**)&d, (size_t)size));
         NR_CHECK(hipMemcpyAsync(d, buffer, (size_t)size, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_u8_to_f64, dim3(grid_for(size)), dim3(256), 0, s, d, t->buffer, size);
         NR_CHECK(hipGetLastError());
-        NR_CHECK(hipFreeAsync(d, s));
+        NR_CHECK(hipStreamSynchronize(s));
+        NR_CHECK(hipFree(d));
     }
     NR_CHECK(hipStreamSynchronize(s));
     return t;

@@ -79,6 +79,7 @@ struct RenderContext {
     u64 fragTotal = 0;
     int lastPath = 0;                 // raster of the last triangle batch (1 order-free, 2 ordered)
     int forceOrdered = 0;             // testing: always take the ordered raster
+    iu8* u8buf = nullptr; size_t u8cap = 0;   // GetBufferAsUInt8 staging
 };
 
 struct Texture {

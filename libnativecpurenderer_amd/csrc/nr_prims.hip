@@ -175,14 +175,16 @@ static TexSrc tex_source(RenderContext* ctx, Texture* tex) {
     s.ptr = tex->buffer;
     if (tex->buffer == ctx->buffer) {
         size_t bytes = (size_t)(tex->width * tex->height * (tex->enableAlpha ? 4 : 3)) * sizeof(f64);
-        NR_CHECK(hipMallocAsync((void**)&s.tmp, bytes, ctx->stream));
+        NR_CHECK(hipMalloc((void**)&s.tmp, bytes));
         NR_CHECK(hipMemcpyAsync(s.tmp, tex->buffer, bytes, hipMemcpyDeviceToDevice, ctx->stream));
         s.ptr = s.tmp;
     }
     return s;
 }
 static void tex_release(RenderContext* ctx, TexSrc& s) {
-    if (s.tmp) NR_CHECK(hipFreeAsync(s.tmp, ctx->stream));
+    if (!s.tmp) return;
+    NR_CHECK(hipStreamSynchronize(ctx->stream));   // rare path: a texture aliasing its own target
+    NR_CHECK(hipFree(s.tmp));
 }
 
 // Fast-path loop bounds of cpp:741-742: i from (i64)x while (f64)i < x + w,

@@ -152,9 +152,10 @@ class OracleContext:
     def draw_triangles(self, xy, rgba, z=None, gouraud=None):
         xy = np.ascontiguousarray(xy, dtype=np.float64).reshape(-1, 6)
         n = xy.shape[0]
-        rgba = np.ascontiguousarray(rgba, dtype=np.float64).reshape(n, -1)
+        rgba = np.ascontiguousarray(rgba, dtype=np.float64)
         if gouraud is None:
-            gouraud = rgba.shape[1] == 12
+            gouraud = rgba.size == 12 * n and n > 0
+        rgba = rgba.reshape(n, 12 if gouraud else 4)
         zp = None
         if z is not None:
             z = np.ascontiguousarray(z, dtype=np.float64).reshape(n, 3)
