@@ -63,6 +63,22 @@ def algorithmic_bytes(cfg, n_tri):
     return n_tri * s_tri + cfg["W"] * cfg["H"] * (8 * 3 + zw)
 
 
+KERNEL_SYMBOL = {"tile_raster": "k_vis / k_tile_raster", "resolve": "k_resolve"}
+
+
+def kernel_bytes(cfg, n_tri, path):
+    """Algorithmic bytes each hot kernel must move per launch:
+    order-free path: k_vis reads each triangle's positions and depths once
+    (48 + 24 B); k_resolve writes the framebuffer and depth once
+    (W*H*(8*ipp + 4)).  Ordered path: k_tile_raster does both, plus colours."""
+    W, H = cfg["W"], cfg["H"]
+    zw = 4 if cfg.get("write", True) else 0
+    fb = W * H * (8 * 3 + zw)
+    if path == "order-free":
+        return {"tile_raster": n_tri * (48 + 24), "resolve": fb}
+    return {"tile_raster": algorithmic_bytes(cfg, n_tri)}
+
+
 def cpu_baseline(cfg, xy, z, c, budget_s=10.0, max_frames=50):
     """The oracle (CPU restatement, single thread) on the same frames."""
     import scenes
@@ -161,13 +177,17 @@ def main():
 
     ms = dt / args.steps * 1e3
     kernels = {}
-    for name in ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "tile_raster", "fill"):
+    for name in ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "vis_init", "tile_raster",
+                 "resolve", "fill"):
         tot, cnt = ctx.get_kernel_timing(name)
         if cnt:
             kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
-    raster_us = kernels.get("tile_raster")
+    path = ctx.last_raster_path()
+    kb = kernel_bytes(cfg, n_tri, path)
+    dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
+    dom_us = kernels[dom]
+    achieved = kb[dom] / (dom_us * 1e-6) / 1e9
     B = algorithmic_bytes(cfg, n_tri)
-    achieved = B / (raster_us * 1e-6) / 1e9 if raster_us else None
     traffic, pmc = load_pmc_traffic(args.config)
 
     if rank != 0:
@@ -189,12 +209,16 @@ def main():
         "config": {"workload": cfg["desc"], "width": W, "height": H, "triangles": n_tri,
                    "fragments_per_frame": int(frags), "frame_pixels": W * H,
                    "parallelism": f"tile-row x{world}" if world > 1 else "single GPU"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None,
+                     "frac": round(achieved / PEAK_HBM_GBPS, 4),
                      "traffic": traffic,
-                     "kernel": "k_tile_raster", "algorithmic_bytes_per_launch": B,
+                     "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
+                     "algorithmic_bytes_per_launch": kb[dom],
+                     "frame_algorithmic_bytes": B,
+                     "frame_achieved": round(B / (ms * 1e-3) / 1e9, 1),
                      "frame_frac": round(B / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)},
+        "raster_path": path,
         "kernel_us": kernels,
     }
     if not args.no_cpu_baseline and world == 1:

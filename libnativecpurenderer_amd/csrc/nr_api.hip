@@ -246,8 +246,9 @@ static void timing_collect(RenderContext* ctx) {
     ctx->evPending.clear();
 }
 
-static const char* kKernelNames[NRK_COUNT_] = {"tri_count", "tri_scan", "tri_emit", "tri_sort",
-                                               "tile_ranges", "tile_raster", "prim", "fill"};
+static const char* kKernelNames[NRK_COUNT_] = {"tri_count", "tri_scan",    "tri_emit", "tri_sort",
+                                               "tile_ranges", "tile_raster", "prim",     "fill",
+                                               "resolve",   "vis_init"};
 
 extern "C" {
 
@@ -290,7 +291,8 @@ void DestroyRenderContext(RenderContext* ctx) {
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
-                    t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf};
+                    t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
+                    t.fcnt,      t.foff,       t.fsoff,    t.fcur, t.flist, t.vis,  t.dplan};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));
@@ -652,7 +654,7 @@ void EnableKernelTiming(RenderContext* ctx, bool on) {
 }
 
 // Sum and count of the named kernel's durations since the last reset
-// (names: tri_count tri_scan tri_emit tri_sort tile_ranges tile_raster prim fill).
+// (names: tri_count tri_scan tri_emit tri_sort tile_ranges tile_raster prim fill resolve vis_init).
 bool GetKernelTiming(RenderContext* ctx, const char* name, f64* total_ms, i64* count) {
     NR_CHECK(hipSetDevice(ctx->device));
     timing_collect(ctx);

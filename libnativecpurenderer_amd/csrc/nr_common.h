@@ -43,11 +43,16 @@ struct TriScratch {
     u64* h_total = nullptr;                 // pinned readback: [0] pairs, [1] last count, [2] fragments
     u64* d_frag = nullptr;                  // device fragment counter
     u32* d_flag = nullptr;                  // device non-opaque flag
+    // visibility-buffer raster (nr_tri_free.hip)
+    u32* fcnt = nullptr; u32* foff = nullptr; u32* fsoff = nullptr; u32* fcur = nullptr; size_t ftile_cap = 0;
+    u32* flist = nullptr; size_t flist_cap = 0;
+    u64* vis = nullptr; size_t vis_cap = 0;
+    u32* dplan = nullptr;
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
 };
 
 enum NRKernelId { NRK_TRI_COUNT = 0, NRK_TRI_SCAN, NRK_TRI_EMIT, NRK_TRI_SORT, NRK_TILE_RANGES,
-                  NRK_TILE_RASTER, NRK_PRIM, NRK_FILL, NRK_COUNT_ };
+                  NRK_TILE_RASTER, NRK_PRIM, NRK_FILL, NRK_RESOLVE, NRK_VIS_INIT, NRK_COUNT_ };
 
 struct RenderContext {
     i64 width = 0, height = 0;

@@ -1,0 +1,155 @@
+// nr_tri.h — shared pieces of the triangle / depth / Gouraud path.
+//
+// Semantics (no reference implementation exists; defined
+// in the reference's idiom, DESIGN.md §3, restated by the CPU oracle):
+//   vertices -> context transform (cpp:446-453) -> screen space;
+//   coverage = even-odd pointInPolygon (cpp:822-845) at integer pixels;
+//   w1,w2 barycentric in f64, attr = a0 + (a1-a0)*w1 + (a2-a0)*w2;
+//   depth u32 LESS, written only when test+write are on;
+//   blend = ApplyPixel (cpp:515-549) in submission order.
+//
+// Two rasterisers share the screen tiling (64x32 tiles) and these helpers:
+//   nr_tri_ordered.hip  in-order tile raster (any batch: blending, Z w/o write)
+//   nr_tri_free.hip     visibility-buffer raster (opaque batches: every
+//                       fragment overwrites, so per-pixel results are an
+//                       order-independent min/max over packed keys)
+#pragma once
+
+#include "nr_common.h"
+
+namespace nrtri {
+
+constexpr int TW = 64;   // tile width  (= one wave's lanes)
+constexpr int TH = 32;   // tile height
+
+struct TriSrc {
+    const f64* xy;    // n*6
+    const f64* z;     // n*3 or null
+    const f64* rgba;  // n*4 flat / n*12 Gouraud
+    int gouraud;
+    i64 n;
+};
+
+struct BinParams {
+    TriSrc src;
+    f64 m[6];
+    i64 W, H;
+    int tiles_x;
+};
+
+__device__ __forceinline__ f64 clampd(f64 v, f64 lo, f64 hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Screen-space vertices of triangle t (cpp:446-453 applied to each vertex).
+__device__ __forceinline__ void tri_screen(const TriSrc& s, const f64* m, i64 t, f64 (&sx)[3], f64 (&sy)[3]) {
+    const f64* p = s.xy + t * 6;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) nr_xform(m, p[2 * v], p[2 * v + 1], sx[v], sy[v]);
+}
+
+__device__ __forceinline__ bool tri_finite(const f64 (&sx)[3], const f64 (&sy)[3]) {
+    return isfinite(sx[0]) && isfinite(sy[0]) && isfinite(sx[1]) && isfinite(sy[1]) && isfinite(sx[2]) &&
+           isfinite(sy[2]);
+}
+
+// Tile rectangle touched by a triangle; false if it produces no fragment.
+// Rows: a row y has a straddling edge iff ymin <= y < ymax (exact), so
+// [ceil(ymin), ceil(ymax)).  Columns: crossings lie in [xmin, xmax] up to
+// rounding, so [floor(xmin)-2, ceil(xmax)+2]; for |coord| > 1e7 the full width.
+__device__ __forceinline__ bool tri_tiles(const f64 (&sx)[3], const f64 (&sy)[3], i64 W, i64 H, int& tx0, int& tx1,
+                                          int& ty0, int& ty1) {
+    bool huge = false;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) huge = huge || fabs(sx[v]) > 1e7 || fabs(sy[v]) > 1e7;
+    if (!tri_finite(sx, sy)) return false;
+    const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+    const f64 den = e1x * e2y - e2x * e1y;
+    if (den == 0) return false;
+    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+    const i64 r0 = (i64)clampd(ceil(ymn), 0.0, (f64)H);
+    const i64 r1 = (i64)clampd(ceil(ymx), 0.0, (f64)H);
+    if (r0 >= r1) return false;
+    i64 c0 = 0, c1 = W - 1;
+    if (!huge) {
+        const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
+        if (ceil(xmx) + 2 < 0 || floor(xmn) - 2 > (f64)(W - 1)) return false;
+        c0 = (i64)clampd(floor(xmn) - 2, 0.0, (f64)(W - 1));
+        c1 = (i64)clampd(ceil(xmx) + 2, 0.0, (f64)(W - 1));
+    }
+    tx0 = (int)(c0 / TW); tx1 = (int)(c1 / TW);
+    ty0 = (int)(r0 / TH); ty1 = (int)((r1 - 1) / TH);
+    return true;
+}
+
+// Exact covered columns [xs, xe) of screen row y, relative to x0 and clamped
+// to [0, wlim].  The two edges straddling y (pointInPolygon's edge order
+// (i=0,j=2) (i=1,j=0) (i=2,j=1) and crossing expression, cpp:832-839) give
+// crossings ca, cb; (x < ca) != (x < cb)  <=>  ceil(min) <= x < ceil(max).
+__device__ __forceinline__ void row_span(const f64 (&sx)[3], const f64 (&sy)[3], f64 y, f64 x0, f64 wlim, int& xs,
+                                         int& xe) {
+    f64 c0 = 0, c1 = 0;
+    int nc = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int j = (i + 2) % 3;
+        if ((sy[i] > y) != (sy[j] > y)) {
+            const f64 cc = (sx[j] - sx[i]) * (y - sy[i]) / (sy[j] - sy[i]) + sx[i];
+            if (nc == 0) c0 = cc; else c1 = cc;
+            ++nc;
+        }
+    }
+    xs = xe = 0;
+    if (nc == 2) {
+        const f64 lo = fmin(c0, c1), hi = fmax(c0, c1);
+        xs = (int)clampd(ceil(lo) - x0, 0.0, wlim);
+        xe = (int)clampd(ceil(hi) - x0, 0.0, wlim);
+        if (xe < xs) xe = xs;
+    }
+}
+
+// State snapshot of one draw call (passed by value to the kernels).
+struct FrameParams {
+    TriSrc src;
+    f64 m[6];
+    f64 ct[4];
+    f64* fb;
+    u32* depth;
+    i64 W, H;
+    int ipp;
+    int tiles_x, tiles_y;
+    int depthTest, depthWrite;
+    int pendColor;
+    f64 pendColorValue;
+    int pendDepth;
+    u32 pendDepthValue;
+    unsigned long long* fragCounter;   // non-null: count covered fragments
+};
+
+enum Opacity { OPQ_UNKNOWN = 0, OPQ_OPAQUE, OPQ_BLENDED };
+
+template <typename T, size_t K>
+bool grow_set(T* (&ptrs)[K], size_t* cap, size_t need) {
+    if (*cap >= need && ptrs[0]) return true;
+    size_t n = need > *cap * 3 / 2 ? need : *cap * 3 / 2;
+    for (size_t k = 0; k < K; ++k) {
+        if (ptrs[k]) NR_CHECK(hipFree(ptrs[k]));
+        ptrs[k] = nullptr;
+    }
+    for (size_t k = 0; k < K; ++k)
+        if (hipMalloc((void**)&ptrs[k], n * sizeof(T)) != hipSuccess) {
+            nr_set_error_msg("triangle scratch: hipMalloc failed");
+            *cap = 0;
+            return false;
+        }
+    *cap = n;
+    return true;
+}
+bool grow_temp(TriScratch& sc, size_t need);
+
+FrameParams frame_params(RenderContext* ctx, const TriSrc& src);
+void finish_batch(RenderContext* ctx, const FrameParams& fp);
+
+// the two rasterisers (host side)
+void draw_ordered(RenderContext* ctx, const TriSrc& src);
+void draw_free(RenderContext* ctx, const TriSrc& src);
+
+}  // namespace nrtri

@@ -1,0 +1,499 @@
+// nr_tri_free.hip — visibility-buffer raster for opaque batches.
+//
+// When every fragment of a batch overwrites (every vertex alpha == 1 and
+// colourTransform[3] == 1, so ApplyPixel's `a != 1` blend never runs) the
+// sequential semantics reduce, per pixel, to an order-independent reduction:
+//   Z LESS + write : winner = min over (zq, tri) with zq < z_init -> min of
+//                    the packed key (zq << 32) | (tri + 1), init z_init << 32
+//   Z LESS, no write: winner = last tri with zq < z_init            -> max id
+//   no Z test       : winner = last covering tri                     -> max id
+// Ties on zq resolve to the lower triangle index = the earlier submission,
+// exactly as the sequential LESS test would.  So fragments are reduced in any
+// order, with 64-bit LDS atomics, and only the winner is shaded (deferred).
+//
+//   1 k_free_count   tile histogram of (tile, triangle) pairs, aggregated in
+//                    LDS per workgroup (one global atomic per touched tile)
+//   2 k_free_plan    one workgroup: exclusive scans of the tile counts (list
+//                    offsets) and of the slice counts (work items)
+//   3 k_free_emit    per-tile lists (order inside a list is irrelevant here)
+//   4 k_vis          one 256-thread workgroup per (tile, slice of <= 512
+//                    triangles): exact row spans -> prefix sum -> fragment-
+//                    parallel depth + LDS atomicMin on the tile's 2048 keys ->
+//                    one coalesced store (or global atomicMin when a long list
+//                    is split over several slices: the load-balancing step for
+//                    mesh poles where thousands of tiny triangles meet)
+//   5 k_resolve      one thread per pixel: winner -> barycentrics -> colour ->
+//                    ApplyPixel -> framebuffer + depth written once; tiles
+//                    with no triangle just receive a pending clear
+#include "nr_tri.h"
+
+namespace nrtri {
+namespace {
+
+constexpr int VWG = 256;     // k_vis workgroup
+constexpr int FCH = 128;     // triangles staged per chunk in k_vis
+constexpr u32 SLICE = 512;   // triangles per work item
+constexpr int TPT = 4;       // triangles per thread in the binning kernels
+constexpr int LDS_HIST_MAX = 16384;
+
+template <bool LDSH>
+__global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __restrict__ tile_cnt, int ntiles) {
+    extern __shared__ u32 hist[];
+    const int tid = threadIdx.x;
+    if (LDSH) {
+        for (int b = tid; b < ntiles; b += 256) hist[b] = 0;
+        __syncthreads();
+    }
+    const i64 base = (i64)blockIdx.x * 256 * TPT;
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        if (t >= bp.src.n) break;
+        f64 sx[3], sy[3];
+        tri_screen(bp.src, bp.m, t, sx, sy);
+        int tx0, tx1, ty0, ty1;
+        if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
+        for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) {
+                const int bin = ty * bp.tiles_x + tx;
+                if (LDSH) atomicAdd(&hist[bin], 1u);
+                else atomicAdd(&tile_cnt[bin], 1u);
+            }
+    }
+    if (LDSH) {
+        __syncthreads();
+        for (int b = tid; b < ntiles; b += 256) {
+            const u32 h = hist[b];
+            if (h) atomicAdd(&tile_cnt[b], h);
+        }
+    }
+}
+
+// Single workgroup: off[i] = sum(cnt[<i]), soff[i] = sum(ceil(cnt[<i]/SLICE)),
+// off[ntiles] = P, soff[ntiles] = number of work items; totals = {P, items,
+// number of tiles split over more than one slice}.
+__global__ __launch_bounds__(1024) void k_free_plan(const u32* __restrict__ cnt, int ntiles, u32* __restrict__ off,
+                                                    u32* __restrict__ soff, u32* __restrict__ totals) {
+    __shared__ u32 sA[1024], sB[1024], sC[1024];
+    const int tid = threadIdx.x;
+    const int per = (ntiles + 1023) / 1024;
+    const int b0 = tid * per, b1 = min(b0 + per, ntiles);
+    u32 a = 0, b = 0, m = 0;
+    for (int i = b0; i < b1; ++i) {
+        const u32 c = cnt[i];
+        a += c;
+        b += (c + SLICE - 1) / SLICE;
+        m += c > SLICE ? 1u : 0u;
+    }
+    sA[tid] = a; sB[tid] = b; sC[tid] = m;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const u32 va = tid >= d ? sA[tid - d] : 0u;
+        const u32 vb = tid >= d ? sB[tid - d] : 0u;
+        const u32 vc = tid >= d ? sC[tid - d] : 0u;
+        __syncthreads();
+        sA[tid] += va; sB[tid] += vb; sC[tid] += vc;
+        __syncthreads();
+    }
+    u32 ea = sA[tid] - a, eb = sB[tid] - b;
+    for (int i = b0; i < b1; ++i) {
+        const u32 c = cnt[i];
+        off[i] = ea;
+        soff[i] = eb;
+        ea += c;
+        eb += (c + SLICE - 1) / SLICE;
+    }
+    if (tid == 1023) {
+        off[ntiles] = sA[1023];
+        soff[ntiles] = sB[1023];
+        totals[0] = sA[1023];
+        totals[1] = sB[1023];
+        totals[2] = sC[1023];
+    }
+}
+
+template <bool LDSH>
+__global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32* __restrict__ off,
+                                                   u32* __restrict__ cur, u32* __restrict__ list, int ntiles) {
+    extern __shared__ u32 hist[];
+    const int tid = threadIdx.x;
+    const i64 base = (i64)blockIdx.x * 256 * TPT;
+    if (LDSH) {
+        for (int b = tid; b < ntiles; b += 256) hist[b] = 0;
+        __syncthreads();
+        for (int k = 0; k < TPT; ++k) {
+            const i64 t = base + k * 256 + tid;
+            if (t >= bp.src.n) break;
+            f64 sx[3], sy[3];
+            tri_screen(bp.src, bp.m, t, sx, sy);
+            int tx0, tx1, ty0, ty1;
+            if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
+            for (int ty = ty0; ty <= ty1; ++ty)
+                for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * bp.tiles_x + tx], 1u);
+        }
+        __syncthreads();
+        // reserve each touched tile's range once: hist[b] becomes the next slot
+        for (int b = tid; b < ntiles; b += 256) {
+            const u32 h = hist[b];
+            if (h) hist[b] = off[b] + atomicAdd(&cur[b], h);
+        }
+        __syncthreads();
+    }
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        if (t >= bp.src.n) break;
+        f64 sx[3], sy[3];
+        tri_screen(bp.src, bp.m, t, sx, sy);
+        int tx0, tx1, ty0, ty1;
+        if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
+        for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) {
+                const int bin = ty * bp.tiles_x + tx;
+                const u32 slot = LDSH ? atomicAdd(&hist[bin], 1u) : off[bin] + atomicAdd(&cur[bin], 1u);
+                list[slot] = (u32)t;
+            }
+    }
+}
+
+// Neutral keys for tiles whose list is split over several slices (their
+// slices merge with global atomics).
+template <int ZMODE>
+__global__ __launch_bounds__(256) void k_vis_init_multi(const FrameParams fp, const u32* __restrict__ off,
+                                                        u64* __restrict__ vis) {
+    const int tile = blockIdx.x;
+    if (off[tile + 1] - off[tile] <= SLICE) return;
+    const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
+    const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
+    for (int p = threadIdx.x; p < TW * TH; p += 256) {
+        const i64 px = x0 + (p & (TW - 1)), py = y0 + p / TW;
+        if (px < fp.W && py < fp.H) vis[py * fp.W + px] = ZMODE == 1 ? ~0ull : 0ull;
+    }
+}
+
+enum { F_X0 = 0, F_Y0, F_E1X, F_E1Y, F_E2X, F_E2Y, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
+
+template <int ZMODE, bool COUNT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+__global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __restrict__ off,
+                                             const u32* __restrict__ soff, const u32* __restrict__ list,
+                                             u64* __restrict__ vis) {
+    constexpr bool DEPTH = ZMODE != 0;
+    __shared__ u64 key[TH * TW];
+    __shared__ u32 zin[ZMODE == 2 ? TH * TW : 1];
+    __shared__ f64 S[F_NSLOT][FCH];
+    __shared__ u32 TIDX[FCH];
+    __shared__ iu8 XS[FCH][TH], XE[FCH][TH];
+    __shared__ u32 OFF[FCH + 1];
+    __shared__ iu8 RR0[FCH];
+    __shared__ int sTile;
+    const int tid = threadIdx.x;
+    const int ntiles = fp.tiles_x * fp.tiles_y;
+    const u32 item = blockIdx.x;
+    if (tid == 0) {   // tile of this work item: last tile with soff[tile] <= item
+        int lo = 0, hi = ntiles;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (soff[mid] <= item) lo = mid; else hi = mid;
+        }
+        sTile = lo;
+    }
+    __syncthreads();
+    const int tile = sTile;
+    const u32 t0 = off[tile], t1 = off[tile + 1];
+    const u32 slice = item - soff[tile];
+    const u32 ls = t0 + slice * SLICE;
+    const u32 le = ls + SLICE < t1 ? ls + SLICE : t1;
+    const bool multi = t1 - t0 > SLICE;
+    const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
+    const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
+    const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
+    const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
+
+    for (int p = tid; p < TH * TW; p += VWG) {
+        const int lx = p & (TW - 1), ly = p / TW;
+        u32 z0 = 0xFFFFFFFFu;
+        if (DEPTH && lx < wlim && ly < hlim)
+            z0 = fp.pendDepth ? fp.pendDepthValue : fp.depth[(y0 + ly) * fp.W + x0 + lx];
+        key[p] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
+        if (ZMODE == 2) zin[p] = z0;
+    }
+    u64 fragTotal = 0;
+
+    for (u32 base = ls; base < le; base += FCH) {
+        const int cnt = (le - base) < (u32)FCH ? (int)(le - base) : FCH;
+        __syncthreads();
+        // ---- (a) setup + exact spans, one thread per triangle
+        if (tid < cnt) {
+            const u32 t = list[base + tid];
+            f64 sx[3], sy[3];
+            tri_screen(fp.src, fp.m, t, sx, sy);
+            const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+            const f64 den = e1x * e2y - e2x * e1y;
+            const bool ok = tri_finite(sx, sy) && den != 0;
+            S[F_X0][tid] = sx[0]; S[F_Y0][tid] = sy[0];
+            S[F_E1X][tid] = e1x; S[F_E1Y][tid] = e1y; S[F_E2X][tid] = e2x; S[F_E2Y][tid] = e2y;
+            S[F_INV][tid] = 1.0 / den;
+            if (DEPTH) {
+                f64 z0 = 0, z1 = 0, z2 = 0;
+                if (fp.src.z) { z0 = fp.src.z[(i64)t * 3]; z1 = fp.src.z[(i64)t * 3 + 1]; z2 = fp.src.z[(i64)t * 3 + 2]; }
+                S[F_Z0][tid] = z0; S[F_DZ1][tid] = z1 - z0; S[F_DZ2][tid] = z2 - z0;
+            }
+            TIDX[tid] = t;
+            int r0 = 0;
+            u32 nf = 0;
+            if (ok) {
+                const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+                r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
+                const int r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
+                for (int r = r0; r < r1; ++r) {
+                    int xs, xe;
+                    row_span(sx, sy, (f64)(y0 + r), (f64)x0, (f64)wlim, xs, xe);
+                    XS[tid][r] = (iu8)xs;
+                    XE[tid][r] = (iu8)xe;
+                    nf += (u32)(xe - xs);
+                }
+            }
+            RR0[tid] = (iu8)r0;
+            OFF[tid] = nf;
+        }
+        __syncthreads();
+        // ---- (b) exclusive scan of the fragment counts (wave 0)
+        if (tid < 64) {
+            constexpr int PER = FCH / 64;
+            u32 v[PER];
+            u32 sum = 0;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int idx = tid * PER + i;
+                v[i] = idx < cnt ? OFF[idx] : 0u;
+                sum += v[i];
+            }
+            u32 incl = sum;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const u32 o = __shfl_up(incl, d, 64);
+                if (tid >= d) incl += o;
+            }
+            u32 ex = incl - sum;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                OFF[tid * PER + i] = ex;
+                ex += v[i];
+            }
+            if (tid == 63) OFF[FCH] = incl;
+        }
+        __syncthreads();
+        // ---- (c) fragment-parallel visibility
+        const u32 F = OFF[cnt];
+        if (COUNT) fragTotal += F;
+        for (u32 f = tid; f < F; f += VWG) {
+            int lo = 0, hi = cnt;   // OFF[lo] <= f < OFF[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (OFF[mid] <= f) lo = mid; else hi = mid;
+            }
+            const int k = lo;
+            u32 l = f - OFF[k];
+            int r = RR0[k];
+            for (;;) {
+                const u32 len = (u32)(XE[k][r] - XS[k][r]);
+                if (l < len) break;
+                l -= len;
+                ++r;
+            }
+            const int lx = XS[k][r] + (int)l;
+            const int p = r * TW + lx;
+            const u64 id1 = (u64)TIDX[k] + 1;
+            if (ZMODE == 0) {
+                atomicMax(&key[p], id1);
+            } else {
+                const f64 dx = (f64)(x0 + lx) - S[F_X0][k], dy = (f64)(y0 + r) - S[F_Y0][k];
+                const f64 w1 = (dx * S[F_E2Y][k] - S[F_E2X][k] * dy) * S[F_INV][k];
+                const f64 w2 = (S[F_E1X][k] * dy - dx * S[F_E1Y][k]) * S[F_INV][k];
+                const f64 zz = S[F_Z0][k] + S[F_DZ1][k] * w1 + S[F_DZ2][k] * w2;
+                const u32 zq = nr_quantize_depth(zz);
+                if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
+                else if (zq < zin[p]) atomicMax(&key[p], id1);
+            }
+        }
+    }
+    __syncthreads();
+    for (int p = tid; p < TH * TW; p += VWG) {
+        const int lx = p & (TW - 1), ly = p / TW;
+        if (lx >= wlim || ly >= hlim) continue;
+        u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
+        if (!multi) *g = key[p];
+        else if (ZMODE == 1) atomicMin(g, key[p]);
+        else atomicMax(g, key[p]);
+    }
+    if (COUNT && tid == 0) atomicAdd(fp.fragCounter, fragTotal);
+}
+
+// One thread per pixel (2-D grid: x blocks of 256, one row per blockIdx.y).
+template <int ZMODE, bool GOURAUD>
+__global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32* __restrict__ off,
+                                                 const u64* __restrict__ vis) {
+    const i64 px = (i64)blockIdx.x * 256 + threadIdx.x;
+    const i64 py = blockIdx.y;
+    if (px >= fp.W) return;
+    const int tile = (int)(py / TH) * fp.tiles_x + (int)(px / TW);
+    const i64 p = py * fp.W + px;
+    const int ipp = fp.ipp;
+    f64* dst = fp.fb + p * ipp;
+    if (off[tile + 1] == off[tile]) {   // no triangle touches this tile
+        if (fp.pendColor) {
+            const f64 v = fp.pendColorValue;
+            dst[0] = v; dst[1] = v; dst[2] = v;
+            if (ipp == 4) dst[3] = v;
+        }
+        if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+        return;
+    }
+    const u64 kv = vis[p];
+    const u32 id1 = (u32)kv;
+    if (id1 == 0) {
+        if (fp.pendColor) {
+            const f64 v = fp.pendColorValue;
+            dst[0] = v; dst[1] = v; dst[2] = v;
+            if (ipp == 4) dst[3] = v;
+        }
+        if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+        return;
+    }
+    f64 R, G, B, A = 0;
+    if (fp.pendColor) {
+        R = G = B = A = fp.pendColorValue;
+    } else {
+        R = dst[0]; G = dst[1]; B = dst[2];
+        if (ipp == 4) A = dst[3];
+    }
+    const i64 t = (i64)id1 - 1;
+    f64 cr, cg, cb, ca;
+    if (GOURAUD) {
+        f64 sx[3], sy[3];
+        tri_screen(fp.src, fp.m, t, sx, sy);
+        const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+        const f64 inv = 1.0 / (e1x * e2y - e2x * e1y);
+        const f64 dx = (f64)px - sx[0], dy = (f64)py - sy[0];
+        const f64 w1 = (dx * e2y - e2x * dy) * inv;
+        const f64 w2 = (e1x * dy - dx * e1y) * inv;
+        const f64* c = fp.src.rgba + t * 12;
+        cr = c[0] + (c[4] - c[0]) * w1 + (c[8] - c[0]) * w2;
+        cg = c[1] + (c[5] - c[1]) * w1 + (c[9] - c[1]) * w2;
+        cb = c[2] + (c[6] - c[2]) * w1 + (c[10] - c[2]) * w2;
+        ca = c[3] + (c[7] - c[3]) * w1 + (c[11] - c[3]) * w2;
+    } else {
+        const f64* c = fp.src.rgba + t * 4;
+        cr = c[0]; cg = c[1]; cb = c[2]; ca = c[3];
+    }
+    // ApplyPixel (cpp:529-547); ca * ct3 == 1 for every batch routed here
+    cr *= fp.ct[0]; cg *= fp.ct[1]; cb *= fp.ct[2]; ca *= fp.ct[3];
+    if (ca != 1) {
+        cr = R * (1 - ca) + cr * ca;
+        cg = G * (1 - ca) + cg * ca;
+        cb = B * (1 - ca) + cb * ca;
+    }
+    dst[0] = cr; dst[1] = cg; dst[2] = cb;
+    if (ipp == 4) dst[3] = ca;
+    if (ZMODE == 1) fp.depth[p] = (u32)(kv >> 32);
+    else if (ZMODE == 2 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+}
+
+template <int Z, bool C>
+void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u32* list, u64* vis, u32 items,
+                hipStream_t s) {
+    hipLaunchKernelGGL((k_vis<Z, C>), dim3(items), dim3(VWG), 0, s, fp, off, soff, list, vis);
+}
+
+template <int Z, bool G>
+void launch_resolve(const FrameParams& fp, const u32* off, const u64* vis, hipStream_t s) {
+    dim3 grid((unsigned)((fp.W + 255) / 256), (unsigned)fp.H);
+    hipLaunchKernelGGL((k_resolve<Z, G>), grid, dim3(256), 0, s, fp, off, vis);
+}
+
+}  // namespace
+
+void draw_free(RenderContext* ctx, const TriSrc& src) {
+    hipStream_t s = ctx->stream;
+    TriScratch& sc = ctx->tri;
+    FrameParams fp = frame_params(ctx, src);
+    const int ntiles = fp.tiles_x * fp.tiles_y;
+    const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
+    const bool g = src.gouraud != 0;
+
+    BinParams bp;
+    bp.src = src;
+    for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
+    bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
+
+    u32* tb[4] = {sc.fcnt, sc.foff, sc.fsoff, sc.fcur};
+    if (!grow_set(tb, &sc.ftile_cap, (size_t)ntiles + 1)) return;
+    sc.fcnt = tb[0]; sc.foff = tb[1]; sc.fsoff = tb[2]; sc.fcur = tb[3];
+    if (!sc.dplan) NR_CHECK(hipMalloc(&sc.dplan, 4 * sizeof(u32)));
+    NR_CHECK(hipMemsetAsync(sc.fcnt, 0, (size_t)ntiles * sizeof(u32), s));
+    NR_CHECK(hipMemsetAsync(sc.fcur, 0, (size_t)ntiles * sizeof(u32), s));
+
+    const bool ldsh = ntiles <= LDS_HIST_MAX;
+    const size_t hbytes = ldsh ? (size_t)ntiles * sizeof(u32) : 0;
+    const int gb = (int)((src.n + 256 * TPT - 1) / (256 * TPT));
+    hipEvent_t e0, e1;
+    nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
+    if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.fcnt, ntiles);
+    else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, s, bp, sc.fcnt, ntiles);
+    NR_CHECK(hipGetLastError());
+    nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
+
+    nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
+    hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, sc.foff, sc.fsoff, sc.dplan);
+    NR_CHECK(hipGetLastError());
+    nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
+
+    // pair and work-item totals: size the list and the k_vis grid (host sync)
+    u32* hp = reinterpret_cast<u32*>(sc.h_total);
+    NR_CHECK(hipMemcpyAsync(hp, sc.dplan, 3 * sizeof(u32), hipMemcpyDeviceToHost, s));
+    NR_CHECK(hipStreamSynchronize(s));
+    const u32 P = hp[0], items = hp[1], multi = hp[2];
+
+    if (P > 0) {
+        u32* lb[1] = {sc.flist};
+        if (!grow_set(lb, &sc.flist_cap, (size_t)P)) return;
+        sc.flist = lb[0];
+        u64* vb[1] = {sc.vis};
+        if (!grow_set(vb, &sc.vis_cap, (size_t)(ctx->width * ctx->height))) return;
+        sc.vis = vb[0];
+
+        nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
+        if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, sc.flist, ntiles);
+        else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, sc.flist, ntiles);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
+
+        if (multi) {
+            nr_timing_begin(ctx, NRK_VIS_INIT, &e0, &e1);
+            if (zmode == 1) hipLaunchKernelGGL(k_vis_init_multi<1>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis);
+            else hipLaunchKernelGGL(k_vis_init_multi<0>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis);
+            NR_CHECK(hipGetLastError());
+            nr_timing_end(ctx, NRK_VIS_INIT, e0, e1);
+        }
+
+        nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
+        const bool C = fp.fragCounter != nullptr;
+        if (zmode == 1) { if (C) launch_vis<1, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<1, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
+        else if (zmode == 2) { if (C) launch_vis<2, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<2, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
+        else { if (C) launch_vis<0, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<0, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+    }
+
+    if (P > 0 || fp.pendColor || (zmode != 0 && fp.pendDepth)) {
+        nr_timing_begin(ctx, NRK_RESOLVE, &e0, &e1);
+        const u64* vis = sc.vis ? sc.vis : reinterpret_cast<const u64*>(sc.foff);   // unread when P == 0
+        if (zmode == 1) { if (g) launch_resolve<1, true>(fp, sc.foff, vis, s); else launch_resolve<1, false>(fp, sc.foff, vis, s); }
+        else if (zmode == 2) { if (g) launch_resolve<2, true>(fp, sc.foff, vis, s); else launch_resolve<2, false>(fp, sc.foff, vis, s); }
+        else { if (g) launch_resolve<0, true>(fp, sc.foff, vis, s); else launch_resolve<0, false>(fp, sc.foff, vis, s); }
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_RESOLVE, e0, e1);
+    }
+    ctx->lastPath = 1;
+    finish_batch(ctx, fp);
+}
+
+}  // namespace nrtri

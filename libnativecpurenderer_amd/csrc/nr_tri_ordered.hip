@@ -1,0 +1,352 @@
+// nr_tri_ordered.hip — in-order tiled raster: correct for every batch
+// (alpha blending, Z test without write, colour transforms), the general
+// path behind DrawTriangles*.
+//
+//   1 k_tri_count   per triangle: number of 64x32 tiles its bbox touches
+//   2 scan          exclusive sum of the counts (hipcub)
+//   3 k_tri_emit    (tile, triangle) pairs, written in triangle order
+//   4 sort          stable radix sort by tile: each tile's list stays in
+//                   submission order (painter's order is preserved)
+//   5 k_tile_ranges start/end of each tile's list
+//   6 k_tile_raster one 512-thread workgroup per tile; the tile's colour and
+//                   Z live in registers (8 waves x 4 rows x 64 lanes) for the
+//                   whole list.  Per 64-triangle chunk the setup and the exact
+//                   per-row coverage spans are staged in LDS, then each wave
+//                   walks the chunk in order and blends its covered lanes
+//                   (ApplyPixel, cpp:529-547).  The tile is read once and
+//                   written once; a pending uniform clear is applied on chip.
+#include "nr_tri.h"
+
+#include <hipcub/hipcub.hpp>
+
+namespace nrtri {
+namespace {
+
+constexpr int RPW = 4;           // rows per wave
+constexpr int NWAVE = TH / RPW;  // 8
+constexpr int WG = NWAVE * 64;   // 512 threads
+constexpr int CH = 64;           // triangles staged per chunk
+
+__global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt) {
+    const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (t >= bp.src.n) return;
+    f64 sx[3], sy[3];
+    tri_screen(bp.src, bp.m, t, sx, sy);
+    int tx0, tx1, ty0, ty1;
+    unsigned long long c = 0;
+    if (tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) c = (unsigned long long)(tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+    cnt[t] = c;
+}
+
+__global__ __launch_bounds__(256) void k_tri_emit(const BinParams bp, const unsigned long long* __restrict__ off,
+                                                  u32* __restrict__ keys, u32* __restrict__ vals) {
+    const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
+    if (t >= bp.src.n) return;
+    f64 sx[3], sy[3];
+    tri_screen(bp.src, bp.m, t, sx, sy);
+    int tx0, tx1, ty0, ty1;
+    if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) return;
+    unsigned long long o = off[t];
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+            keys[o] = (u32)(ty * bp.tiles_x + tx);
+            vals[o] = (u32)t;
+            ++o;
+        }
+}
+
+__global__ __launch_bounds__(256) void k_tile_ranges(const u32* __restrict__ keys, u32 P, u32* __restrict__ start,
+                                                     u32* __restrict__ end) {
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    const u32 k = keys[i];
+    if (i == 0 || keys[i - 1] != k) start[k] = i;
+    if (i == P - 1 || keys[i + 1] != k) end[k] = i + 1;
+}
+
+// LDS staging slots of a chunk (SoA, CH entries each)
+enum {
+    S_X0 = 0, S_Y0, S_X1, S_Y1, S_X2, S_Y2,   // screen-space vertices
+    S_E1X, S_E1Y, S_E2X, S_E2Y, S_INV,         // barycentric setup
+    S_Z0, S_DZ1, S_DZ2,                        // depth: z0, z1-z0, z2-z0
+    S_C0,                                      // colour c0[4] (flat: the colour)
+    S_D1 = S_C0 + 4,                           // c1-c0 [4] (Gouraud)
+    S_D2 = S_D1 + 4,                           // c2-c0 [4] (Gouraud)
+    S_NSLOT = S_D2 + 4
+};
+
+template <bool GOURAUD, bool DEPTH, bool COUNT>
+__global__ __launch_bounds__(WG) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
+                                                    const u32* __restrict__ tstart, const u32* __restrict__ tend) {
+    const int tile = blockIdx.x;
+    const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
+    const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const u32 ls = tstart[tile], le = tend[tile];
+    if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
+
+    __shared__ f64 S[S_NSLOT][CH];
+    __shared__ iu8 XS[CH][TH], XE[CH][TH];
+    __shared__ iu8 NE[CH][NWAVE];
+    __shared__ iu8 VALID[CH];
+    __shared__ unsigned long long fragSum;
+    if (COUNT && tid == 0) fragSum = 0;
+
+    // ---- the tile's pixel state, resident in registers for the whole list
+    const i64 px = x0 + lane;
+    const int ipp = fp.ipp;
+    f64 cr[RPW], cg[RPW], cb[RPW], ca[RPW];
+    u32 cz[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const i64 py = y0 + wave * RPW + r;
+        cr[r] = cg[r] = cb[r] = ca[r] = 0;
+        cz[r] = 0xFFFFFFFFu;
+        if (px < fp.W && py < fp.H) {
+            if (fp.pendColor) {
+                cr[r] = cg[r] = cb[r] = ca[r] = fp.pendColorValue;
+            } else {
+                const f64* p = fp.fb + (py * fp.W + px) * ipp;
+                cr[r] = p[0]; cg[r] = p[1]; cb[r] = p[2];
+                if (ipp == 4) ca[r] = p[3];
+            }
+            if (DEPTH) cz[r] = fp.pendDepth ? fp.pendDepthValue : fp.depth[py * fp.W + px];
+        }
+    }
+    const f64 ct0 = fp.ct[0], ct1 = fp.ct[1], ct2 = fp.ct[2], ct3 = fp.ct[3];
+    const f64 wlim = (f64)(fp.W - x0 < TW ? fp.W - x0 : TW);
+    unsigned long long myFrags = 0;
+
+    for (u32 base = ls; base < le; base += CH) {
+        const int cnt = (le - base) < (u32)CH ? (int)(le - base) : CH;
+        // ---- (a) triangle setup, one thread per triangle
+        if (tid < cnt) {
+            const i64 t = list[base + tid];
+            f64 sx[3], sy[3];
+            tri_screen(fp.src, fp.m, t, sx, sy);
+            const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+            const f64 den = e1x * e2y - e2x * e1y;
+            VALID[tid] = tri_finite(sx, sy) && den != 0;
+            S[S_X0][tid] = sx[0]; S[S_Y0][tid] = sy[0];
+            S[S_X1][tid] = sx[1]; S[S_Y1][tid] = sy[1];
+            S[S_X2][tid] = sx[2]; S[S_Y2][tid] = sy[2];
+            S[S_E1X][tid] = e1x; S[S_E1Y][tid] = e1y; S[S_E2X][tid] = e2x; S[S_E2Y][tid] = e2y;
+            S[S_INV][tid] = 1.0 / den;
+            if (DEPTH) {
+                f64 z0 = 0, z1 = 0, z2 = 0;
+                if (fp.src.z) { z0 = fp.src.z[t * 3]; z1 = fp.src.z[t * 3 + 1]; z2 = fp.src.z[t * 3 + 2]; }
+                S[S_Z0][tid] = z0; S[S_DZ1][tid] = z1 - z0; S[S_DZ2][tid] = z2 - z0;
+            }
+            if (GOURAUD) {
+                const f64* c = fp.src.rgba + t * 12;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    S[S_C0 + k][tid] = c[k];
+                    S[S_D1 + k][tid] = c[4 + k] - c[k];
+                    S[S_D2 + k][tid] = c[8 + k] - c[k];
+                }
+            } else {
+                const f64* c = fp.src.rgba + t * 4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) S[S_C0 + k][tid] = c[k];
+            }
+        }
+        __syncthreads();
+        // ---- (b) exact coverage spans: thread = (triangle k, wave-row group rg)
+        {
+            const int k = tid >> 3, rg = tid & 7;
+            if (k < cnt) {
+                bool any = false;
+                const bool ok = VALID[k];
+                const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
+                const f64 sy[3] = {S[S_Y0][k], S[S_Y1][k], S[S_Y2][k]};
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    const int row = rg * RPW + r;
+                    const i64 gy = y0 + row;
+                    int xs = 0, xe = 0;
+                    if (ok && gy < fp.H) row_span(sx, sy, (f64)gy, (f64)x0, wlim, xs, xe);
+                    XS[k][row] = (iu8)xs;
+                    XE[k][row] = (iu8)xe;
+                    any = any || xs < xe;
+                    if (COUNT) myFrags += (unsigned long long)(xe - xs);
+                }
+                NE[k][rg] = any;
+            }
+        }
+        __syncthreads();
+        // ---- (c) in-order raster of the chunk; each wave owns 4 rows
+        for (int k = 0; k < cnt; ++k) {
+            if (!NE[k][wave]) continue;
+            const f64 sx0 = S[S_X0][k], sy0 = S[S_Y0][k];
+            const f64 e1x = S[S_E1X][k], e1y = S[S_E1Y][k], e2x = S[S_E2X][k], e2y = S[S_E2Y][k];
+            const f64 inv = S[S_INV][k];
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int row = wave * RPW + r;
+                const int xs = XS[k][row], xe = XE[k][row];
+                if (lane < xs || lane >= xe) continue;
+                f64 w1 = 0, w2 = 0;
+                if (DEPTH || GOURAUD) {
+                    const f64 dx = (f64)(x0 + lane) - sx0, dy = (f64)(y0 + row) - sy0;
+                    w1 = (dx * e2y - e2x * dy) * inv;
+                    w2 = (e1x * dy - dx * e1y) * inv;
+                }
+                u32 zq = 0;
+                if (DEPTH) {
+                    const f64 zz = S[S_Z0][k] + S[S_DZ1][k] * w1 + S[S_DZ2][k] * w2;
+                    zq = nr_quantize_depth(zz);
+                    if (!(zq < cz[r])) continue;
+                }
+                f64 R, G, B, A;
+                if (GOURAUD) {
+                    R = S[S_C0 + 0][k] + S[S_D1 + 0][k] * w1 + S[S_D2 + 0][k] * w2;
+                    G = S[S_C0 + 1][k] + S[S_D1 + 1][k] * w1 + S[S_D2 + 1][k] * w2;
+                    B = S[S_C0 + 2][k] + S[S_D1 + 2][k] * w1 + S[S_D2 + 2][k] * w2;
+                    A = S[S_C0 + 3][k] + S[S_D1 + 3][k] * w1 + S[S_D2 + 3][k] * w2;
+                } else {
+                    R = S[S_C0 + 0][k]; G = S[S_C0 + 1][k]; B = S[S_C0 + 2][k]; A = S[S_C0 + 3][k];
+                }
+                // ApplyPixel (cpp:529-547) on the register-resident pixel
+                R *= ct0; G *= ct1; B *= ct2; A *= ct3;
+                if (A != 1) {
+                    R = cr[r] * (1 - A) + R * A;
+                    G = cg[r] * (1 - A) + G * A;
+                    B = cb[r] * (1 - A) + B * A;
+                }
+                cr[r] = R; cg[r] = G; cb[r] = B; ca[r] = A;
+                if (DEPTH && fp.depthWrite) cz[r] = zq;
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- write the tile back once
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const i64 py = y0 + wave * RPW + r;
+        if (px < fp.W && py < fp.H) {
+            f64* p = fp.fb + (py * fp.W + px) * ipp;
+            p[0] = cr[r]; p[1] = cg[r]; p[2] = cb[r];
+            if (ipp == 4) p[3] = ca[r];
+            if (DEPTH && (fp.depthWrite || fp.pendDepth)) fp.depth[py * fp.W + px] = cz[r];
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&fragSum, myFrags);
+        __syncthreads();
+        if (tid == 0) atomicAdd(fp.fragCounter, fragSum);
+    }
+}
+
+template <bool G, bool D, bool C>
+void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s) {
+    hipLaunchKernelGGL((k_tile_raster<G, D, C>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te);
+}
+
+template <bool C>
+void launch_raster_c(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles,
+                     hipStream_t s) {
+    const bool g = fp.src.gouraud != 0, d = fp.depthTest != 0;
+    if (g && d) launch_raster<true, true, C>(fp, list, ts, te, ntiles, s);
+    else if (g) launch_raster<true, false, C>(fp, list, ts, te, ntiles, s);
+    else if (d) launch_raster<false, true, C>(fp, list, ts, te, ntiles, s);
+    else launch_raster<false, false, C>(fp, list, ts, te, ntiles, s);
+}
+
+}  // namespace
+
+void draw_ordered(RenderContext* ctx, const TriSrc& src) {
+    hipStream_t s = ctx->stream;
+    TriScratch& sc = ctx->tri;
+    FrameParams fp = frame_params(ctx, src);
+    const int ntiles = fp.tiles_x * fp.tiles_y;
+
+    BinParams bp;
+    bp.src = src;
+    for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
+    bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
+
+    u64* tri_bufs[2] = {sc.cnt, sc.off};
+    if (!grow_set(tri_bufs, &sc.tri_cap, (size_t)src.n)) return;
+    sc.cnt = tri_bufs[0]; sc.off = tri_bufs[1];
+    u32* tile_bufs[2] = {sc.tile_start, sc.tile_end};
+    if (!grow_set(tile_bufs, &sc.tile_cap, (size_t)ntiles)) return;
+    sc.tile_start = tile_bufs[0]; sc.tile_end = tile_bufs[1];
+
+    const int g1 = (int)((src.n + 255) / 256);
+    hipEvent_t e0, e1;
+    nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
+    hipLaunchKernelGGL(k_tri_count, dim3(g1), dim3(256), 0, s, bp, sc.cnt);
+    NR_CHECK(hipGetLastError());
+    nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
+
+    size_t need = 0;
+    NR_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, sc.cnt, sc.off, (int)src.n, s));
+    if (!grow_temp(sc, need)) return;
+    nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
+    NR_CHECK(hipcub::DeviceScan::ExclusiveSum(sc.temp, need, sc.cnt, sc.off, (int)src.n, s));
+    nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
+
+    // total pair count: sizes the sort (host sync)
+    NR_CHECK(hipMemcpyAsync(&sc.h_total[0], sc.off + (src.n - 1), sizeof(u64), hipMemcpyDeviceToHost, s));
+    NR_CHECK(hipMemcpyAsync(&sc.h_total[1], sc.cnt + (src.n - 1), sizeof(u64), hipMemcpyDeviceToHost, s));
+    NR_CHECK(hipStreamSynchronize(s));
+    const u64 P = sc.h_total[0] + sc.h_total[1];
+
+    if (P > (1ull << 31) && src.n > 1) {
+        // too many pairs for one pass: split the batch; submission order kept
+        TriSrc a = src, b = src;
+        a.n = src.n / 2;
+        b.n = src.n - a.n;
+        b.xy = src.xy + a.n * 6;
+        b.z = src.z ? src.z + a.n * 3 : nullptr;
+        b.rgba = src.rgba + a.n * (src.gouraud ? 12 : 4);
+        draw_ordered(ctx, a);
+        draw_ordered(ctx, b);
+        return;
+    }
+
+    NR_CHECK(hipMemsetAsync(sc.tile_start, 0, (size_t)ntiles * sizeof(u32), s));
+    NR_CHECK(hipMemsetAsync(sc.tile_end, 0, (size_t)ntiles * sizeof(u32), s));
+
+    const u32* list = sc.tile_start;   // never dereferenced when every list is empty
+    if (P > 0) {
+        u32* pair_bufs[4] = {sc.keys[0], sc.keys[1], sc.vals[0], sc.vals[1]};
+        if (!grow_set(pair_bufs, &sc.pair_cap, (size_t)P)) return;
+        sc.keys[0] = pair_bufs[0]; sc.keys[1] = pair_bufs[1]; sc.vals[0] = pair_bufs[2]; sc.vals[1] = pair_bufs[3];
+
+        nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
+        hipLaunchKernelGGL(k_tri_emit, dim3(g1), dim3(256), 0, s, bp, sc.off, sc.keys[0], sc.vals[0]);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
+
+        int bits = 1;
+        while ((1 << bits) < ntiles) ++bits;
+        size_t sneed = 0;
+        NR_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sneed, sc.keys[0], sc.keys[1], sc.vals[0], sc.vals[1],
+                                                    (int)P, 0, bits, s));
+        if (!grow_temp(sc, sneed)) return;
+        nr_timing_begin(ctx, NRK_TRI_SORT, &e0, &e1);
+        NR_CHECK(hipcub::DeviceRadixSort::SortPairs(sc.temp, sneed, sc.keys[0], sc.keys[1], sc.vals[0], sc.vals[1],
+                                                    (int)P, 0, bits, s));
+        nr_timing_end(ctx, NRK_TRI_SORT, e0, e1);
+
+        nr_timing_begin(ctx, NRK_TILE_RANGES, &e0, &e1);
+        hipLaunchKernelGGL(k_tile_ranges, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, sc.keys[1], (u32)P,
+                           sc.tile_start, sc.tile_end);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TILE_RANGES, e0, e1);
+        list = sc.vals[1];
+    }
+
+    nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
+    if (fp.fragCounter) launch_raster_c<true>(fp, list, sc.tile_start, sc.tile_end, ntiles, s);
+    else launch_raster_c<false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s);
+    NR_CHECK(hipGetLastError());
+    nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+    ctx->lastPath = 2;
+    finish_batch(ctx, fp);
+}
+
+}  // namespace nrtri
