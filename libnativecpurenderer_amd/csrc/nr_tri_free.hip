@@ -243,6 +243,7 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
                 const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
                 r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
                 const int r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
                 for (int r = r0; r < r1; ++r) {
                     int xs, xe;
                     row_span(sx, sy, (f64)(y0 + r), (f64)x0, (f64)wlim, xs, xe);
