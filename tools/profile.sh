@@ -18,10 +18,10 @@ run() {  # name, timeout, args...
 run list 60 rocprofv3 -L
 grep -oE "^[[:space:]]*(SQ_|TCC_|TCP_|GRBM_|FETCH|WRITE)[A-Za-z0-9_]*" $OUT/list.log | sort -u > $OUT/counter_names.txt
 run trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $BENCH --steps 10 --warmup 2
-KR=${KERNEL_REGEX:-k_tile_raster}
-run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $KR -d $OUT/pmc_fetch -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
-run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex $KR -d $OUT/pmc_write -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
-run pmc_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-include-regex $KR -d $OUT/pmc_sq1 -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
-run pmc_sq2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex $KR -d $OUT/pmc_sq2 -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
-run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex $KR -d $OUT/pmc_tcc -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
+KR=${KERNEL_REGEX:-"k_vis|k_resolve|k_tile_raster"}
+run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_fetch -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
+run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_write -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
+run pmc_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-include-regex "$KR" -d $OUT/pmc_sq1 -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
+run pmc_sq2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex "$KR" -d $OUT/pmc_sq2 -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
+run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KR" -d $OUT/pmc_tcc -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
 ls -R $OUT | head -50
