@@ -36,17 +36,6 @@ constexpr u32 SLICE = 512;   // triangles per work item
 constexpr int TPT = 4;       // triangles per thread in the binning kernels
 constexpr int LDS_HIST_MAX = 16384;
 
-// One (tile, triangle) pair as k_vis consumes it: screen-space vertices and
-// depths, written by k_free_emit while it streams the triangles (coalesced),
-// so k_vis reads its chunk contiguously instead of gathering.
-struct alignas(16) PairRec {
-    f64 sx[3], sy[3];
-    f64 z[3];
-    u32 tri;
-    u32 pad;
-};
-static_assert(sizeof(PairRec) == 80, "PairRec layout");
-
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __restrict__ tile_cnt, int ntiles) {
     extern __shared__ u32 hist[];
@@ -124,7 +113,7 @@ __global__ __launch_bounds__(1024) void k_free_plan(const u32* __restrict__ cnt,
 
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32* __restrict__ off,
-                                                   u32* __restrict__ cur, PairRec* __restrict__ rec, int ntiles) {
+                                                   u32* __restrict__ cur, u32* __restrict__ list, int ntiles) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
     const i64 base = (i64)blockIdx.x * 256 * TPT;
@@ -156,19 +145,11 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
         tri_screen(bp.src, bp.m, t, sx, sy);
         int tx0, tx1, ty0, ty1;
         if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
-        f64 z0 = 0, z1 = 0, z2 = 0;
-        if (bp.src.z) { z0 = bp.src.z[t * 3]; z1 = bp.src.z[t * 3 + 1]; z2 = bp.src.z[t * 3 + 2]; }
         for (int ty = ty0; ty <= ty1; ++ty)
             for (int tx = tx0; tx <= tx1; ++tx) {
                 const int bin = ty * bp.tiles_x + tx;
                 const u32 slot = LDSH ? atomicAdd(&hist[bin], 1u) : off[bin] + atomicAdd(&cur[bin], 1u);
-                PairRec r;
-                r.sx[0] = sx[0]; r.sx[1] = sx[1]; r.sx[2] = sx[2];
-                r.sy[0] = sy[0]; r.sy[1] = sy[1]; r.sy[2] = sy[2];
-                r.z[0] = z0; r.z[1] = z1; r.z[2] = z2;
-                r.tri = (u32)t;
-                r.pad = 0;
-                rec[slot] = r;
+                list[slot] = (u32)t;
             }
     }
 }
@@ -192,7 +173,7 @@ enum { F_X0 = 0, F_Y0, F_E1X, F_E1Y, F_E2X, F_E2Y, F_INV, F_Z0, F_DZ1, F_DZ2, F_
 
 template <int ZMODE, bool COUNT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __restrict__ off,
-                                             const u32* __restrict__ soff, const PairRec* __restrict__ rec,
+                                             const u32* __restrict__ soff, const u32* __restrict__ list,
                                              u64* __restrict__ vis) {
     constexpr bool DEPTH = ZMODE != 0;
     __shared__ u64 key[TH * TW];
@@ -241,10 +222,9 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
         __syncthreads();
         // ---- (a) setup + exact spans, one thread per triangle
         if (tid < cnt) {
-            const PairRec rc = rec[base + tid];
-            const u32 t = rc.tri;
-            const f64 sx[3] = {rc.sx[0], rc.sx[1], rc.sx[2]};
-            const f64 sy[3] = {rc.sy[0], rc.sy[1], rc.sy[2]};
+            const u32 t = list[base + tid];
+            f64 sx[3], sy[3];
+            tri_screen(fp.src, fp.m, t, sx, sy);
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
             const f64 den = e1x * e2y - e2x * e1y;
             const bool ok = tri_finite(sx, sy) && den != 0;
@@ -252,7 +232,9 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             S[F_E1X][tid] = e1x; S[F_E1Y][tid] = e1y; S[F_E2X][tid] = e2x; S[F_E2Y][tid] = e2y;
             S[F_INV][tid] = 1.0 / den;
             if (DEPTH) {
-                S[F_Z0][tid] = rc.z[0]; S[F_DZ1][tid] = rc.z[1] - rc.z[0]; S[F_DZ2][tid] = rc.z[2] - rc.z[0];
+                f64 z0 = 0, z1 = 0, z2 = 0;
+                if (fp.src.z) { z0 = fp.src.z[(i64)t * 3]; z1 = fp.src.z[(i64)t * 3 + 1]; z2 = fp.src.z[(i64)t * 3 + 2]; }
+                S[F_Z0][tid] = z0; S[F_DZ1][tid] = z1 - z0; S[F_DZ2][tid] = z2 - z0;
             }
             TIDX[tid] = t;
             int r0 = 0;
@@ -417,9 +399,9 @@ __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32
 }
 
 template <int Z, bool C>
-void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const PairRec* rec, u64* vis, u32 items,
+void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u32* list, u64* vis, u32 items,
                 hipStream_t s) {
-    hipLaunchKernelGGL((k_vis<Z, C>), dim3(items), dim3(VWG), 0, s, fp, off, soff, rec, vis);
+    hipLaunchKernelGGL((k_vis<Z, C>), dim3(items), dim3(VWG), 0, s, fp, off, soff, list, vis);
 }
 
 template <int Z, bool G>
@@ -472,18 +454,16 @@ void draw_free(RenderContext* ctx, const TriSrc& src) {
     const u32 P = hp[0], items = hp[1], multi = hp[2];
 
     if (P > 0) {
-        // pair records (80 B each) live in the flist allocation
         u32* lb[1] = {sc.flist};
-        if (!grow_set(lb, &sc.flist_cap, (size_t)P * (sizeof(PairRec) / sizeof(u32)))) return;
+        if (!grow_set(lb, &sc.flist_cap, (size_t)P)) return;
         sc.flist = lb[0];
-        PairRec* rec = reinterpret_cast<PairRec*>(sc.flist);
         u64* vb[1] = {sc.vis};
         if (!grow_set(vb, &sc.vis_cap, (size_t)(ctx->width * ctx->height))) return;
         sc.vis = vb[0];
 
         nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
-        if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, rec, ntiles);
-        else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, rec, ntiles);
+        if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, sc.flist, ntiles);
+        else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, sc.flist, ntiles);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
 
@@ -497,9 +477,9 @@ void draw_free(RenderContext* ctx, const TriSrc& src) {
 
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool C = fp.fragCounter != nullptr;
-        if (zmode == 1) { if (C) launch_vis<1, true>(fp, sc.foff, sc.fsoff, rec, sc.vis, items, s); else launch_vis<1, false>(fp, sc.foff, sc.fsoff, rec, sc.vis, items, s); }
-        else if (zmode == 2) { if (C) launch_vis<2, true>(fp, sc.foff, sc.fsoff, rec, sc.vis, items, s); else launch_vis<2, false>(fp, sc.foff, sc.fsoff, rec, sc.vis, items, s); }
-        else { if (C) launch_vis<0, true>(fp, sc.foff, sc.fsoff, rec, sc.vis, items, s); else launch_vis<0, false>(fp, sc.foff, sc.fsoff, rec, sc.vis, items, s); }
+        if (zmode == 1) { if (C) launch_vis<1, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<1, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
+        else if (zmode == 2) { if (C) launch_vis<2, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<2, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
+        else { if (C) launch_vis<0, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<0, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
     }
