@@ -169,8 +169,13 @@ __global__ __launch_bounds__(256) void k_vis_init_multi(const FrameParams fp, co
     }
 }
 
-enum { F_X0 = 0, F_Y0, F_E1X, F_E1Y, F_E2X, F_E2Y, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
+enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_E1X, F_E1Y, F_E2X, F_E2Y, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
 
+// Per chunk of FCH triangles: (a) one thread per triangle: setup + the rows
+// of this tile it straddles; (b) exclusive scan of the row counts; (c) the
+// chunk's (triangle, row) items are spread evenly over all threads: one
+// binary search per item, the exact span, then a short per-lane walk over the
+// span's pixels (depth + LDS atomic on the packed key).
 template <int ZMODE, bool COUNT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __restrict__ off,
                                              const u32* __restrict__ soff, const u32* __restrict__ list,
@@ -180,10 +185,10 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     __shared__ u32 zin[ZMODE == 2 ? TH * TW : 1];
     __shared__ f64 S[F_NSLOT][FCH];
     __shared__ u32 TIDX[FCH];
-    __shared__ iu8 XS[FCH][TH], XE[FCH][TH];
-    __shared__ u32 OFF[FCH + 1];
+    __shared__ u32 ROFF[FCH + 1];
     __shared__ iu8 RR0[FCH];
     __shared__ int sTile;
+    __shared__ unsigned long long sFrag;
     const int tid = threadIdx.x;
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const u32 item = blockIdx.x;
@@ -194,6 +199,7 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             if (soff[mid] <= item) lo = mid; else hi = mid;
         }
         sTile = lo;
+        sFrag = 0;
     }
     __syncthreads();
     const int tile = sTile;
@@ -215,12 +221,12 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
         key[p] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
         if (ZMODE == 2) zin[p] = z0;
     }
-    u64 fragTotal = 0;
+    unsigned long long myFrags = 0;
 
     for (u32 base = ls; base < le; base += FCH) {
         const int cnt = (le - base) < (u32)FCH ? (int)(le - base) : FCH;
         __syncthreads();
-        // ---- (a) setup + exact spans, one thread per triangle
+        // ---- (a) setup, one thread per triangle
         if (tid < cnt) {
             const u32 t = list[base + tid];
             f64 sx[3], sy[3];
@@ -229,6 +235,8 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             const f64 den = e1x * e2y - e2x * e1y;
             const bool ok = tri_finite(sx, sy) && den != 0;
             S[F_X0][tid] = sx[0]; S[F_Y0][tid] = sy[0];
+            S[F_X1][tid] = sx[1]; S[F_Y1][tid] = sy[1];
+            S[F_X2][tid] = sx[2]; S[F_Y2][tid] = sy[2];
             S[F_E1X][tid] = e1x; S[F_E1Y][tid] = e1y; S[F_E2X][tid] = e2x; S[F_E2Y][tid] = e2y;
             S[F_INV][tid] = 1.0 / den;
             if (DEPTH) {
@@ -237,26 +245,19 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
                 S[F_Z0][tid] = z0; S[F_DZ1][tid] = z1 - z0; S[F_DZ2][tid] = z2 - z0;
             }
             TIDX[tid] = t;
-            int r0 = 0;
-            u32 nf = 0;
+            int r0 = 0, nr = 0;
             if (ok) {
+                // rows with a straddling edge: ymin <= y < ymax (exact)
                 const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
                 r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
                 const int r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
-#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-                for (int r = r0; r < r1; ++r) {
-                    int xs, xe;
-                    row_span(sx, sy, (f64)(y0 + r), (f64)x0, (f64)wlim, xs, xe);
-                    XS[tid][r] = (iu8)xs;
-                    XE[tid][r] = (iu8)xe;
-                    nf += (u32)(xe - xs);
-                }
+                nr = r1 > r0 ? r1 - r0 : 0;
             }
             RR0[tid] = (iu8)r0;
-            OFF[tid] = nf;
+            ROFF[tid] = (u32)nr;
         }
         __syncthreads();
-        // ---- (b) exclusive scan of the fragment counts (wave 0)
+        // ---- (b) exclusive scan of the row counts (wave 0)
         if (tid < 64) {
             constexpr int PER = FCH / 64;
             u32 v[PER];
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int idx = tid * PER + i;
-                v[i] = idx < cnt ? OFF[idx] : 0u;
+                v[i] = idx < cnt ? ROFF[idx] : 0u;
                 sum += v[i];
             }
             u32 incl = sum;
@@ -276,41 +277,48 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             u32 ex = incl - sum;
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
-                OFF[tid * PER + i] = ex;
+                ROFF[tid * PER + i] = ex;
                 ex += v[i];
             }
-            if (tid == 63) OFF[FCH] = incl;
+            if (tid == 63) ROFF[FCH] = incl;
         }
         __syncthreads();
-        // ---- (c) fragment-parallel visibility
-        const u32 F = OFF[cnt];
-        if (COUNT) fragTotal += F;
-        for (u32 f = tid; f < F; f += VWG) {
-            int lo = 0, hi = cnt;   // OFF[lo] <= f < OFF[hi]
+        // ---- (c) (triangle, row) items over all threads
+        const u32 R = ROFF[cnt];
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+        for (u32 it = tid; it < R; it += VWG) {
+            int lo = 0, hi = cnt;   // ROFF[lo] <= it < ROFF[hi]
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
-                if (OFF[mid] <= f) lo = mid; else hi = mid;
+                if (ROFF[mid] <= it) lo = mid; else hi = mid;
             }
             const int k = lo;
-            u32 l = f - OFF[k];
-            int r = RR0[k];
-            for (;;) {
-                const u32 len = (u32)(XE[k][r] - XS[k][r]);
-                if (l < len) break;
-                l -= len;
-                ++r;
-            }
-            const int lx = XS[k][r] + (int)l;
-            const int p = r * TW + lx;
+            const int r = RR0[k] + (int)(it - ROFF[k]);
+            const f64 sx[3] = {S[F_X0][k], S[F_X1][k], S[F_X2][k]};
+            const f64 sy[3] = {S[F_Y0][k], S[F_Y1][k], S[F_Y2][k]};
+            const f64 y = (f64)(y0 + r);
+            int xs, xe;
+            row_span(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);
+            if (COUNT) myFrags += (unsigned long long)(xe - xs);
+            if (xs >= xe) continue;
             const u64 id1 = (u64)TIDX[k] + 1;
             if (ZMODE == 0) {
-                atomicMax(&key[p], id1);
-            } else {
-                const f64 dx = (f64)(x0 + lx) - S[F_X0][k], dy = (f64)(y0 + r) - S[F_Y0][k];
-                const f64 w1 = (dx * S[F_E2Y][k] - S[F_E2X][k] * dy) * S[F_INV][k];
-                const f64 w2 = (S[F_E1X][k] * dy - dx * S[F_E1Y][k]) * S[F_INV][k];
-                const f64 zz = S[F_Z0][k] + S[F_DZ1][k] * w1 + S[F_DZ2][k] * w2;
+#pragma clang loop vectorize(disable) interleave(disable)
+                for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * TW + lx], id1);
+                continue;
+            }
+            const f64 e1x = S[F_E1X][k], e1y = S[F_E1Y][k], e2x = S[F_E2X][k], e2y = S[F_E2Y][k];
+            const f64 inv = S[F_INV][k];
+            const f64 zz0 = S[F_Z0][k], dz1 = S[F_DZ1][k], dz2 = S[F_DZ2][k];
+            const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
+#pragma clang loop vectorize(disable) interleave(disable)
+            for (int lx = xs; lx < xe; ++lx) {
+                const f64 dx = (f64)(x0 + lx) - sx[0];
+                const f64 w1 = (dx * e2y - e2x * dy) * inv;
+                const f64 w2 = (e1x * dy - dx * e1y) * inv;
+                const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
                 const u32 zq = nr_quantize_depth(zz);
+                const int p = r * TW + lx;
                 if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
                 else if (zq < zin[p]) atomicMax(&key[p], id1);
             }
@@ -325,7 +333,11 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
         else if (ZMODE == 1) atomicMin(g, key[p]);
         else atomicMax(g, key[p]);
     }
-    if (COUNT && tid == 0) atomicAdd(fp.fragCounter, fragTotal);
+    if (COUNT) {
+        atomicAdd(&sFrag, myFrags);
+        __syncthreads();
+        if (tid == 0) atomicAdd(fp.fragCounter, sFrag);
+    }
 }
 
 // One thread per pixel (2-D grid: x blocks of 256, one row per blockIdx.y).
