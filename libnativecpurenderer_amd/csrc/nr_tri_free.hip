@@ -223,14 +223,32 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     }
     unsigned long long myFrags = 0;
 
+    // next chunk's triangle, prefetched into registers during phase (c)
+    u32 pt = 0;
+    f64 pxy[6], pz[3] = {0, 0, 0};
+    auto prefetch = [&](u32 b) {
+        if (b + tid < le && tid < FCH) {
+            pt = list[b + tid];
+            const f64* q = fp.src.xy + (i64)pt * 6;
+#pragma unroll
+            for (int v = 0; v < 6; ++v) pxy[v] = q[v];
+            if (DEPTH && fp.src.z) {
+                const f64* qz = fp.src.z + (i64)pt * 3;
+                pz[0] = qz[0]; pz[1] = qz[1]; pz[2] = qz[2];
+            }
+        }
+    };
+    prefetch(ls);
+
     for (u32 base = ls; base < le; base += FCH) {
         const int cnt = (le - base) < (u32)FCH ? (int)(le - base) : FCH;
         __syncthreads();
         // ---- (a) setup, one thread per triangle
         if (tid < cnt) {
-            const u32 t = list[base + tid];
+            const u32 t = pt;
             f64 sx[3], sy[3];
-            tri_screen(fp.src, fp.m, t, sx, sy);
+#pragma unroll
+            for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
             const f64 den = e1x * e2y - e2x * e1y;
             const bool ok = tri_finite(sx, sy) && den != 0;
@@ -240,9 +258,7 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             S[F_E1X][tid] = e1x; S[F_E1Y][tid] = e1y; S[F_E2X][tid] = e2x; S[F_E2Y][tid] = e2y;
             S[F_INV][tid] = 1.0 / den;
             if (DEPTH) {
-                f64 z0 = 0, z1 = 0, z2 = 0;
-                if (fp.src.z) { z0 = fp.src.z[(i64)t * 3]; z1 = fp.src.z[(i64)t * 3 + 1]; z2 = fp.src.z[(i64)t * 3 + 2]; }
-                S[F_Z0][tid] = z0; S[F_DZ1][tid] = z1 - z0; S[F_DZ2][tid] = z2 - z0;
+                S[F_Z0][tid] = pz[0]; S[F_DZ1][tid] = pz[1] - pz[0]; S[F_DZ2][tid] = pz[2] - pz[0];
             }
             TIDX[tid] = t;
             int r0 = 0, nr = 0;
@@ -257,6 +273,7 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             ROFF[tid] = (u32)nr;
         }
         __syncthreads();
+        prefetch(base + FCH);
         // ---- (b) exclusive scan of the row counts (wave 0)
         if (tid < 64) {
             constexpr int PER = FCH / 64;
@@ -340,13 +357,23 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     }
 }
 
-// One thread per pixel (2-D grid: x blocks of 256, one row per blockIdx.y).
+// One thread per pixel; a 256-thread block covers a 64x4 pixel region (one
+// tile column, 4 rows).  Blocks are dealt round-robin to the 8 XCDs, so the
+// linear block id is remapped: XCD k (= b % 8) takes the k-th eighth of the
+// regions in row-major order, i.e. one horizontal band of the screen, and the
+// winners' triangle data stays in that XCD's L2 instead of being fetched by
+// all eight (speed only; correctness never depends on placement).
 template <int ZMODE, bool GOURAUD>
 __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32* __restrict__ off,
                                                  const u64* __restrict__ vis) {
-    const i64 px = (i64)blockIdx.x * 256 + threadIdx.x;
-    const i64 py = blockIdx.y;
-    if (px >= fp.W) return;
+    const u32 nblk = gridDim.x;
+    const u32 per = (nblk + 7) / 8;
+    const u32 lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    const u32 bands = (u32)((fp.H + 3) / 4);
+    if (lin >= (u32)fp.tiles_x * bands) return;
+    const i64 px = (i64)(lin % fp.tiles_x) * TW + (threadIdx.x & 63);
+    const i64 py = (i64)(lin / fp.tiles_x) * 4 + (threadIdx.x >> 6);
+    if (px >= fp.W || py >= fp.H) return;
     const int tile = (int)(py / TH) * fp.tiles_x + (int)(px / TW);
     const i64 p = py * fp.W + px;
     const int ipp = fp.ipp;
@@ -418,8 +445,9 @@ void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u3
 
 template <int Z, bool G>
 void launch_resolve(const FrameParams& fp, const u32* off, const u64* vis, hipStream_t s) {
-    dim3 grid((unsigned)((fp.W + 255) / 256), (unsigned)fp.H);
-    hipLaunchKernelGGL((k_resolve<Z, G>), grid, dim3(256), 0, s, fp, off, vis);
+    const u32 regions = (u32)fp.tiles_x * (u32)((fp.H + 3) / 4);
+    const u32 grid = (regions + 7) / 8 * 8;   // a multiple of 8: every XCD gets the same share
+    hipLaunchKernelGGL((k_resolve<Z, G>), dim3(grid), dim3(256), 0, s, fp, off, vis);
 }
 
 }  // namespace
