@@ -357,23 +357,13 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     }
 }
 
-// One thread per pixel; a 256-thread block covers a 64x4 pixel region (one
-// tile column, 4 rows).  Blocks are dealt round-robin to the 8 XCDs, so the
-// linear block id is remapped: XCD k (= b % 8) takes the k-th eighth of the
-// regions in row-major order, i.e. one horizontal band of the screen, and the
-// winners' triangle data stays in that XCD's L2 instead of being fetched by
-// all eight (speed only; correctness never depends on placement).
+// One thread per pixel (2-D grid: x blocks of 256, one row per blockIdx.y).
 template <int ZMODE, bool GOURAUD>
 __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32* __restrict__ off,
                                                  const u64* __restrict__ vis) {
-    const u32 nblk = gridDim.x;
-    const u32 per = (nblk + 7) / 8;
-    const u32 lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    const u32 bands = (u32)((fp.H + 3) / 4);
-    if (lin >= (u32)fp.tiles_x * bands) return;
-    const i64 px = (i64)(lin % fp.tiles_x) * TW + (threadIdx.x & 63);
-    const i64 py = (i64)(lin / fp.tiles_x) * 4 + (threadIdx.x >> 6);
-    if (px >= fp.W || py >= fp.H) return;
+    const i64 px = (i64)blockIdx.x * 256 + threadIdx.x;
+    const i64 py = blockIdx.y;
+    if (px >= fp.W) return;
     const int tile = (int)(py / TH) * fp.tiles_x + (int)(px / TW);
     const i64 p = py * fp.W + px;
     const int ipp = fp.ipp;
@@ -445,9 +435,8 @@ void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u3
 
 template <int Z, bool G>
 void launch_resolve(const FrameParams& fp, const u32* off, const u64* vis, hipStream_t s) {
-    const u32 regions = (u32)fp.tiles_x * (u32)((fp.H + 3) / 4);
-    const u32 grid = (regions + 7) / 8 * 8;   // a multiple of 8: every XCD gets the same share
-    hipLaunchKernelGGL((k_resolve<Z, G>), dim3(grid), dim3(256), 0, s, fp, off, vis);
+    dim3 grid((unsigned)((fp.W + 255) / 256), (unsigned)fp.H);
+    hipLaunchKernelGGL((k_resolve<Z, G>), grid, dim3(256), 0, s, fp, off, vis);
 }
 
 }  // namespace
