@@ -105,6 +105,17 @@ i64 GetFragmentCount(RenderContext* ctx);                                /* NEW 
 i64 GetLastRasterPath(RenderContext* ctx);                               /* NEW: 1 order-free, 2 ordered */
 void SetForceOrderedRaster(RenderContext* ctx, bool on);                 /* NEW: A/B and tests */
 
+/* ---- NEW: multi-GPU frames (tile-row sharding + RCCL assembly) */
+typedef struct NrComm NrComm;
+bool GetCommUniqueId(iu8* out128);              /* rank 0: 128-byte RCCL id to distribute */
+NrComm* CreateComm(i64 nranks, i64 rank, const iu8* id128); /* on the current device */
+void DestroyComm(NrComm* comm);
+void SetShard(RenderContext* ctx, i64 nshards, i64 shard);  /* own tile rows ty % nshards == shard */
+bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root);  /* u8 frame (cpp:52-57) assembled on root */
+void GetFrameU8(RenderContext* ctx, iu8* out);
+void* GetFrameU8DevicePtr(RenderContext* ctx);
+bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root); /* f64 + depth bands to root */
+
 /* ---- NEW: device, sync, interop, errors, measurement --------------------- */
 bool SetDevice(i64 device);                      /* device for objects created next on this thread */
 i64 GetDeviceCount(void);

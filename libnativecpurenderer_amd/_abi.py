@@ -89,6 +89,14 @@ DEVICE_ABI = {
     "GetStreamPtr": (P, (P,)),
     "GetBufferAsUInt8Device": (None, (P, P)),
     "GetTextureBuffer": (None, (P, P)),
+    "GetCommUniqueId": (B, (P,)),
+    "CreateComm": (P, (L, L, P)),
+    "DestroyComm": (None, (P,)),
+    "SetShard": (None, (P, L, L)),
+    "GatherFrameU8": (B, (P, P, L)),
+    "GetFrameU8": (None, (P, P)),
+    "GetFrameU8DevicePtr": (P, (P,)),
+    "GatherFramebuffer": (B, (P, P, L)),
     "EnableKernelTiming": (None, (P, B)),
     "GetKernelTiming": (B, (P, ctypes.c_char_p, P, P)),
     "ResetKernelTiming": (None, (P,)),

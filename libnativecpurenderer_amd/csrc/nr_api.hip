@@ -248,7 +248,7 @@ static void timing_collect(RenderContext* ctx) {
 
 static const char* kKernelNames[NRK_COUNT_] = {"tri_count", "tri_scan",    "tri_emit", "tri_sort",
                                                "tile_ranges", "tile_raster", "prim",     "fill",
-                                               "resolve",   "vis_init"};
+                                               "resolve",   "vis_init",    "output",   "gather"};
 
 extern "C" {
 
@@ -292,7 +292,7 @@ void DestroyRenderContext(RenderContext* ctx) {
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
                     t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
-                    t.fcnt,      t.foff,       t.fsoff,    t.fcur, t.flist, t.vis,  t.dplan};
+                    t.fcnt,      t.foff,       t.fsoff,    t.fcur, t.flist, t.vis,  t.dplan, ctx->frameU8};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));

@@ -52,7 +52,8 @@ struct TriScratch {
 };
 
 enum NRKernelId { NRK_TRI_COUNT = 0, NRK_TRI_SCAN, NRK_TRI_EMIT, NRK_TRI_SORT, NRK_TILE_RANGES,
-                  NRK_TILE_RASTER, NRK_PRIM, NRK_FILL, NRK_RESOLVE, NRK_VIS_INIT, NRK_COUNT_ };
+                  NRK_TILE_RASTER, NRK_PRIM, NRK_FILL, NRK_RESOLVE, NRK_VIS_INIT, NRK_OUTPUT, NRK_GATHER,
+                  NRK_COUNT_ };
 
 struct RenderContext {
     i64 width = 0, height = 0;
@@ -85,6 +86,9 @@ struct RenderContext {
     int lastPath = 0;                 // raster of the last triangle batch (1 order-free, 2 ordered)
     int forceOrdered = 0;             // testing: always take the ordered raster
     iu8* u8buf = nullptr; size_t u8cap = 0;   // GetBufferAsUInt8 staging
+    // multi-GPU: owned tile rows ty % nshards == shard (nr_dist.hip)
+    int nshards = 1, shard = 0;
+    iu8* frameU8 = nullptr; size_t frameU8cap = 0;   // assembled u8 frame (GatherFrameU8)
 };
 
 struct Texture {

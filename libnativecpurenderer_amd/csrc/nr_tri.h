@@ -35,7 +35,10 @@ struct BinParams {
     f64 m[6];
     i64 W, H;
     int tiles_x;
+    int nshards, shard;   // owned tile rows: ty % nshards == shard
 };
+
+__device__ __forceinline__ bool owned_row(int ty, int nshards, int shard) { return ty % nshards == shard; }
 
 __device__ __forceinline__ f64 clampd(f64 v, f64 lo, f64 hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
@@ -116,6 +119,7 @@ struct FrameParams {
     i64 W, H;
     int ipp;
     int tiles_x, tiles_y;
+    int nshards, shard;
     int depthTest, depthWrite;
     int pendColor;
     f64 pendColorValue;

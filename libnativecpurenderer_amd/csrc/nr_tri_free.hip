@@ -52,12 +52,14 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
         tri_screen(bp.src, bp.m, t, sx, sy);
         int tx0, tx1, ty0, ty1;
         if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
-        for (int ty = ty0; ty <= ty1; ++ty)
+        for (int ty = ty0; ty <= ty1; ++ty) {
+            if (!owned_row(ty, bp.nshards, bp.shard)) continue;
             for (int tx = tx0; tx <= tx1; ++tx) {
                 const int bin = ty * bp.tiles_x + tx;
                 if (LDSH) atomicAdd(&hist[bin], 1u);
                 else atomicAdd(&tile_cnt[bin], 1u);
             }
+        }
     }
     if (LDSH) {
         __syncthreads();
@@ -128,7 +130,8 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
             int tx0, tx1, ty0, ty1;
             if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
             for (int ty = ty0; ty <= ty1; ++ty)
-                for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * bp.tiles_x + tx], 1u);
+                if (owned_row(ty, bp.nshards, bp.shard))
+                    for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * bp.tiles_x + tx], 1u);
         }
         __syncthreads();
         // reserve each touched tile's range once: hist[b] becomes the next slot
@@ -145,12 +148,14 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
         tri_screen(bp.src, bp.m, t, sx, sy);
         int tx0, tx1, ty0, ty1;
         if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
-        for (int ty = ty0; ty <= ty1; ++ty)
+        for (int ty = ty0; ty <= ty1; ++ty) {
+            if (!owned_row(ty, bp.nshards, bp.shard)) continue;
             for (int tx = tx0; tx <= tx1; ++tx) {
                 const int bin = ty * bp.tiles_x + tx;
                 const u32 slot = LDSH ? atomicAdd(&hist[bin], 1u) : off[bin] + atomicAdd(&cur[bin], 1u);
                 list[slot] = (u32)t;
             }
+        }
     }
 }
 
@@ -362,8 +367,9 @@ template <int ZMODE, bool GOURAUD>
 __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32* __restrict__ off,
                                                  const u64* __restrict__ vis) {
     const i64 px = (i64)blockIdx.x * 256 + threadIdx.x;
-    const i64 py = blockIdx.y;
-    if (px >= fp.W) return;
+    // blockIdx.y enumerates the rows of the owned tile rows only
+    const i64 py = ((i64)(blockIdx.y / TH) * fp.nshards + fp.shard) * TH + blockIdx.y % TH;
+    if (px >= fp.W || py >= fp.H) return;
     const int tile = (int)(py / TH) * fp.tiles_x + (int)(px / TW);
     const i64 p = py * fp.W + px;
     const int ipp = fp.ipp;
@@ -435,7 +441,9 @@ void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u3
 
 template <int Z, bool G>
 void launch_resolve(const FrameParams& fp, const u32* off, const u64* vis, hipStream_t s) {
-    dim3 grid((unsigned)((fp.W + 255) / 256), (unsigned)fp.H);
+    const int owned = (fp.tiles_y - fp.shard + fp.nshards - 1) / fp.nshards;
+    if (owned <= 0) return;
+    dim3 grid((unsigned)((fp.W + 255) / 256), (unsigned)(owned * TH));
     hipLaunchKernelGGL((k_resolve<Z, G>), grid, dim3(256), 0, s, fp, off, vis);
 }
 
@@ -453,6 +461,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src) {
     bp.src = src;
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
+    bp.nshards = fp.nshards; bp.shard = fp.shard;
 
     u32* tb[4] = {sc.fcnt, sc.foff, sc.fsoff, sc.fcur};
     if (!grow_set(tb, &sc.ftile_cap, (size_t)ntiles + 1)) return;

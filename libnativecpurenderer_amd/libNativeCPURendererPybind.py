@@ -285,6 +285,28 @@ class RenderContext:
     def get_fragment_count(self) -> int:
         return lib.GetFragmentCount(self._ptr)
 
+    # ---- additions: multi-GPU frames ----------------------
+    def set_shard(self, nshards: int, shard: int):
+        """Render only the 32-pixel tile rows ty with ty % nshards == shard."""
+        lib.SetShard(self._ptr, nshards, shard)
+
+    def gather_frame_u8(self, comm: typing.Optional["Comm"] = None, root: int = 0):
+        """u8 image of the frame assembled on `root` (local conversion when
+        comm is None).  Asynchronous; read it with get_frame_u8()."""
+        if not lib.GatherFrameU8(self._ptr, comm._ptr if comm is not None else None, root):
+            raise RuntimeError("GatherFrameU8 failed: " + _lib.last_error())
+
+    def get_frame_u8(self) -> np.ndarray:
+        ipp = 4 if self.enable_alpha else 3
+        out = np.empty((self.height, self.width, ipp), dtype=np.uint8)
+        lib.GetFrameU8(self._ptr, out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+    def gather_framebuffer(self, comm: "Comm", root: int = 0):
+        """f64 framebuffer (+ depth) bands of every rank assembled on `root`."""
+        if not lib.GatherFramebuffer(self._ptr, comm._ptr, root):
+            raise RuntimeError("GatherFramebuffer failed: " + _lib.last_error())
+
     def last_raster_path(self) -> str:
         return {0: "none", 1: "order-free", 2: "ordered"}[lib.GetLastRasterPath(self._ptr)]
 
@@ -385,6 +407,29 @@ class TriangleBuffer:
         if getattr(self, "_can_release", False):
             lib.DestroyTriangleBuffer(self._ptr)
             self._can_release = False
+
+
+class Comm:
+    """RCCL communicator (one rank per process/GPU) used to assemble sharded
+    frames.  Rank 0 creates the id with Comm.unique_id() and every rank passes
+    the same 128 bytes (e.g. via torch.distributed) to the constructor."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_ubyte * 128)()
+        if not lib.GetCommUniqueId(buf):
+            raise RuntimeError("GetCommUniqueId failed: " + _lib.last_error())
+        return bytes(buf)
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        buf = (ctypes.c_ubyte * 128).from_buffer_copy(uid)
+        self.nranks, self.rank = nranks, rank
+        self._ptr = _check(lib.CreateComm(nranks, rank, buf), "CreateComm")
+
+    def __del__(self):
+        if getattr(self, "_ptr", None):
+            lib.DestroyComm(self._ptr)
+            self._ptr = None
 
 
 def get_version():

@@ -164,3 +164,61 @@ def test_order_free_equals_ordered(gpu, mode, gouraud):
         assert ctx.last_raster_path() == ("ordered" if force else "order-free")
         outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
     assert_same(outs[0], outs[1], f"free-vs-ordered {mode} g={gouraud}")
+
+
+def _bands(H, n, r, th=32):
+    """Rows owned by shard r of n (tile rows ty % n == r)."""
+    return [y for y in range(H) if (y // th) % n == r]
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+@pytest.mark.parametrize("opaque", [True, False])
+def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, opaque):
+    """Every shard renders only its tile rows; the owned rows of all shards
+    put together are byte-identical to the unsharded frame (colour + depth),
+    for both rasterisers; fragment counts add up."""
+    W, H = 333, 250
+    alpha = None if opaque else (0.3, 0.9)
+    xy, z, c = scenes.triangle_soup(3000, W, H, 18, seed=41, gouraud=True, alpha=alpha)
+
+    def render(n, r):
+        ctx = gpu.context(W, H, False)
+        ctx.set_shard(n, r)
+        ctx.set_color(0.1, 0.1, 0.1, 0.1)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.set_fragment_counting(True)
+        ctx.draw_triangles(xy, c, z=z)
+        ctx.gather_frame_u8()           # local conversion of the owned rows
+        return ctx.get_buffer_numpy(), ctx.get_depth_buffer(), ctx.get_frame_u8(), ctx.get_fragment_count()
+
+    full, fullz, fullu8, fullfrags = render(1, 0)
+    asm, asmz, asmu8 = np.zeros_like(full), np.zeros_like(fullz), np.zeros_like(fullu8)
+    frags = 0
+    for r in range(nshards):
+        f, zz, u8, fr = render(nshards, r)
+        rows = _bands(H, nshards, r)
+        asm[rows], asmz[rows], asmu8[rows] = f[rows], zz[rows], u8[rows]
+        frags += fr
+    assert scenes.bits_equal(asm, full)
+    assert np.array_equal(asmz, fullz)
+    assert np.array_equal(asmu8, fullu8)
+    assert frags == fullfrags
+    ctx = gpu.context(W, H, False)
+    ctx.set_color(0.1, 0.1, 0.1, 0.1)
+    ctx.set_depth_state(True, True)
+    ctx.clear_depth()
+    ctx.draw_triangles(xy, c, z=z)
+    assert np.array_equal(fullu8, ctx.get_buffer_as_uint8_numpy())
+
+
+def test_single_rank_comm_gather(gpu):
+    """The RCCL path with a one-rank communicator (a no-op assembly)."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    comm = R.Comm(1, 0, R.Comm.unique_id())
+    ctx = gpu.context(100, 70, True)
+    ctx.set_color(0, 0, 0, 0)
+    ctx.draw_rect(10, 10, 50, 30, 0.5, 0.25, 1.0, 1.0)
+    ctx.gather_frame_u8(comm, 0)
+    ctx.gather_framebuffer(comm, 0)
+    assert np.array_equal(ctx.get_frame_u8(), ctx.get_buffer_as_uint8_numpy())
