@@ -9,10 +9,13 @@ triangles already resident in HBM.  The work unit is a covered on-screen
 pixel x triangle pair (counted once, outside the timed region, by the
 library's fragment counter; equal to the oracle's count — tests check it).
 
-Multi-GPU (torchrun, one process per GPU): the frame's 32-pixel tile rows are
-owned round-robin by the ranks; every rank bins and rasterises only its rows
-(no data-path collective), then the owned rows are gathered to rank 0 over
-RCCL.  value = frame fragments / max-over-ranks time.
+Every step ends with the frame output: the u8 image (cpp:52-57, what the
+video writer consumes) assembled on rank 0.  Multi-GPU (torchrun, one process
+per GPU): the frame's 32-pixel tile rows are owned round-robin by the ranks;
+every rank bins and rasterises only its rows (no data-path collective), then
+its rows of the u8 image go to rank 0 in one grouped RCCL send/recv over xGMI
+(DESIGN.md §5).  At N=1 the same step runs with a local conversion.
+value = frame fragments (summed over ranks) x steps / max-over-ranks time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -136,19 +139,29 @@ def main():
     n_tri = len(xy)
     ctx = R.RenderContext(W, H, False)
     buf = R.TriangleBuffer(xy, c, z=z, gouraud=cfg["gouraud"])
+    comm = None
+    if world > 1:
+        from libnativecpurenderer_amd import sharding
+        ctx.set_shard(world, rank)
+        comm = sharding.make_comm(dist, world, rank)
 
     def frame():
         ctx.set_color(0, 0, 0, 0)
         ctx.set_depth_state(True, cfg.get("write", True))
         ctx.clear_depth()
         ctx.draw_triangle_buffer(buf)
+        ctx.gather_frame_u8(comm, 0)
 
-    # fragment count of one frame (outside the timed region)
+    # fragment count of one frame (outside the timed region), summed over ranks
     ctx.set_fragment_counting(True)
     frame()
     ctx.flush()
     frags = ctx.get_fragment_count()
     ctx.set_fragment_counting(False)
+    if dist is not None:
+        t = torch.tensor([frags], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        frags = int(t.item())
 
     for _ in range(args.warmup):
         frame()
@@ -178,7 +191,7 @@ def main():
     ms = dt / args.steps * 1e3
     kernels = {}
     for name in ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "vis_init", "tile_raster",
-                 "resolve", "fill"):
+                 "resolve", "fill", "output", "gather"):
         tot, cnt = ctx.get_kernel_timing(name)
         if cnt:
             kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
@@ -208,7 +221,8 @@ def main():
         "data": "synthetic (deterministic displaced UV sphere / seeded soup, SURVEY.md §8d)",
         "config": {"workload": cfg["desc"], "width": W, "height": H, "triangles": n_tri,
                    "fragments_per_frame": int(frags), "frame_pixels": W * H,
-                   "parallelism": f"tile-row x{world}" if world > 1 else "single GPU"},
+                   "parallelism": (f"tile-row shards x{world} + RCCL u8 frame gather" if world > 1
+                                   else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBPS, 4),
