@@ -184,6 +184,7 @@ void nr_ensure_depth(RenderContext* ctx) {
 void nr_materialize_color(RenderContext* ctx) {
     if (!ctx->pendColor) return;
     ctx->pendColor = false;
+    ctx->frameU8Valid = false;
     hipEvent_t a, b;
     nr_timing_begin(ctx, NRK_FILL, &a, &b);
     nr_fill_f64(ctx->stream, ctx->buffer, ctx->width * ctx->height * (ctx->enableAlpha ? 4 : 3),
@@ -306,6 +307,7 @@ void DestroyRenderContext(RenderContext* ctx) {
 
 // cpp:39-45 (new buffer; content unspecified in the reference, zeroed here)
 void ResizeRenderContext(RenderContext* ctx, i64 width, i64 height) {
+    ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     NR_CHECK(hipFree(ctx->buffer));
@@ -540,6 +542,7 @@ void ApplyColorTransform(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
 // cpp:494-513 (single-pixel store incl. the RGB overrun into index+3)
 bool SetPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
     if (x < 0 || x >= ctx->width || y < 0 || y >= ctx->height) return false;
+    ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
     i64 ipp = ctx->enableAlpha ? 4 : 3;
@@ -557,6 +560,7 @@ __global__ void k_apply_one(f64* p, int ipp, f64 r, f64 g, f64 b, f64 a, f64 c0,
 }
 bool ApplyPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
     if (x < 0 || x >= ctx->width || y < 0 || y >= ctx->height) return false;
+    ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
     int ipp = ctx->enableAlpha ? 4 : 3;
@@ -568,6 +572,7 @@ bool ApplyPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
 
 // cpp:643-657
 void SetColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
+    ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
     if (r == g && g == b && b == a) {
         // uniform clear: kept pending, consumed on chip by the tiled raster
@@ -605,6 +610,7 @@ void GetColor(RenderContext* ctx, f64 x, f64 y, f64* r, f64* g, f64* b, f64* a) 
 
 // cpp:682-691
 void FillColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
+    ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
     i64 n = ctx->width * ctx->height;

@@ -166,7 +166,10 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
     const i64 rowElems = ctx->width * ipp;
     const i64 bands = (ctx->height + BAND - 1) / BAND;
     const i64 owned = (bands - ctx->shard + ctx->nshards - 1) / ctx->nshards;
-    if (owned > 0) {
+    // later triangle resolves write the u8 frame themselves (no re-read of
+    // the f64 frame); convert here only when that mirror is not current
+    ctx->frameOutput = true;
+    if (owned > 0 && !ctx->frameU8Valid) {
         dim3 grid((unsigned)std::min<i64>((BAND * rowElems + 255) / 256, 4096), (unsigned)owned);
         hipEvent_t e0, e1;
         nr_timing_begin(ctx, NRK_OUTPUT, &e0, &e1);
@@ -175,6 +178,7 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_OUTPUT, e0, e1);
     }
+    ctx->frameU8Valid = true;
     if (!comm || comm->nranks == 1) return true;
     if (comm->nranks != ctx->nshards || comm->rank != ctx->shard) {
         nr_set_error_msg("GatherFrameU8: the context's shard must match the communicator (SetShard(nranks, rank))");

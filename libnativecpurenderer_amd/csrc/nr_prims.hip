@@ -160,6 +160,7 @@ static void launch(RenderContext* ctx, PrimParams& p, i64 i0, i64 i1, i64 j0, i6
 static void prepare(RenderContext* ctx) {
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
+    ctx->frameU8Valid = false;
 }
 
 // Texture source for a draw.  An alias of the destination framebuffer is read

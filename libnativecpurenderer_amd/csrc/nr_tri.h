@@ -126,6 +126,7 @@ struct FrameParams {
     int pendDepth;
     u32 pendDepthValue;
     unsigned long long* fragCounter;   // non-null: count covered fragments
+    iu8* frameU8;                      // non-null: resolve also writes the u8 frame (cpp:52-57)
 };
 
 enum Opacity { OPQ_UNKNOWN = 0, OPQ_OPAQUE, OPQ_BLENDED };

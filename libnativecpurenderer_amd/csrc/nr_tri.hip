@@ -49,6 +49,7 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src) {
     fp.pendDepth = ctx->depthTest && ctx->pendDepth;
     fp.pendDepthValue = ctx->pendDepthValue;
     fp.fragCounter = nullptr;
+    fp.frameU8 = nullptr;
     if (ctx->countFragments) {
         if (!sc.d_frag) NR_CHECK(hipMalloc(&sc.d_frag, sizeof(u64)));
         NR_CHECK(hipMemsetAsync(sc.d_frag, 0, sizeof(u64), ctx->stream));
@@ -60,6 +61,9 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src) {
 // After the raster: account fragments, and mark the deferred clears consumed.
 void finish_batch(RenderContext* ctx, const FrameParams& fp) {
     TriScratch& sc = ctx->tri;
+    // the u8 mirror is current only when this batch's resolve wrote it for
+    // every owned pixel (it does exactly when a clear was pending)
+    ctx->frameU8Valid = fp.frameU8 != nullptr;
     if (fp.fragCounter) {
         NR_CHECK(hipMemcpyAsync(&sc.h_total[2], sc.d_frag, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
         NR_CHECK(hipStreamSynchronize(ctx->stream));

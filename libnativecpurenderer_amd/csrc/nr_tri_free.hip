@@ -374,11 +374,17 @@ __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32
     const i64 p = py * fp.W + px;
     const int ipp = fp.ipp;
     f64* dst = fp.fb + p * ipp;
+    iu8* d8 = fp.frameU8 ? fp.frameU8 + p * ipp : nullptr;
     if (off[tile + 1] == off[tile]) {   // no triangle touches this tile
         if (fp.pendColor) {
             const f64 v = fp.pendColorValue;
             dst[0] = v; dst[1] = v; dst[2] = v;
             if (ipp == 4) dst[3] = v;
+            if (d8) {
+                const iu8 v8 = nr_to_u8(v);
+                d8[0] = v8; d8[1] = v8; d8[2] = v8;
+                if (ipp == 4) d8[3] = v8;
+            }
         }
         if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
         return;
@@ -390,6 +396,11 @@ __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32
             const f64 v = fp.pendColorValue;
             dst[0] = v; dst[1] = v; dst[2] = v;
             if (ipp == 4) dst[3] = v;
+            if (d8) {
+                const iu8 v8 = nr_to_u8(v);
+                d8[0] = v8; d8[1] = v8; d8[2] = v8;
+                if (ipp == 4) d8[3] = v8;
+            }
         }
         if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
         return;
@@ -429,6 +440,10 @@ __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32
     }
     dst[0] = cr; dst[1] = cg; dst[2] = cb;
     if (ipp == 4) dst[3] = ca;
+    if (d8) {
+        d8[0] = nr_to_u8(cr); d8[1] = nr_to_u8(cg); d8[2] = nr_to_u8(cb);
+        if (ipp == 4) d8[3] = nr_to_u8(ca);
+    }
     if (ZMODE == 1) fp.depth[p] = (u32)(kv >> 32);
     else if (ZMODE == 2 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
 }
@@ -456,6 +471,10 @@ void draw_free(RenderContext* ctx, const TriSrc& src) {
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
     const bool g = src.gouraud != 0;
+    if (ctx->frameOutput && fp.pendColor) {
+        const size_t n = (size_t)(ctx->width * ctx->height * fp.ipp);
+        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
+    }
 
     BinParams bp;
     bp.src = src;

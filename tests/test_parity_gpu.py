@@ -222,3 +222,23 @@ def test_single_rank_comm_gather(gpu):
     ctx.gather_frame_u8(comm, 0)
     ctx.gather_framebuffer(comm, 0)
     assert np.array_equal(ctx.get_frame_u8(), ctx.get_buffer_as_uint8_numpy())
+
+
+def test_fused_frame_output_matches_conversion(gpu):
+    """After the first GatherFrameU8 the resolve writes the u8 frame itself;
+    the mirror must equal GetBufferAsUInt8 every frame, including frames with
+    a second (non-clearing) batch or a primitive drawn after the triangles."""
+    W, H = 300, 200
+    xy, z, c = scenes.triangle_soup(2000, W, H, 15, seed=51, gouraud=True)
+    ctx = gpu.context(W, H, False)
+    for frame in range(4):
+        ctx.set_color(0.05 * frame, 0.05 * frame, 0.05 * frame, 0.05 * frame)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.draw_triangles(xy, c, z=z)
+        if frame == 2:
+            ctx.draw_triangles(xy[:100] + 7.0, c[:100], z=z[:100] * 0.5)
+        if frame == 3:
+            ctx.draw_rect(20, 20, 50, 40, 1, 0, 0, 0.5)
+        ctx.gather_frame_u8()
+        assert np.array_equal(ctx.get_frame_u8(), ctx.get_buffer_as_uint8_numpy()), frame
