@@ -78,6 +78,7 @@ DEVICE_ABI = {
     "GetFragmentCount": (L, (P,)),
     "GetLastRasterPath": (L, (P,)),
     "SetForceOrderedRaster": (None, (P, B)),
+    "SetPairCapacityOverride": (None, (P, L)),
     "GetLastErrorString": (ctypes.c_char_p, ()),
     "ClearLastError": (None, ()),
     "SetDevice": (B, (L,)),

@@ -64,6 +64,23 @@ hipStream_t nr_stream_for(int device) {
     return g_streams[device];
 }
 
+// live contexts (nr_settle_all validates every pending batch)
+static std::mutex g_ctx_mu;
+static std::vector<RenderContext*> g_ctxs;
+
+void nr_settle_all() {
+    std::vector<RenderContext*> v;
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        v = g_ctxs;
+    }
+    for (RenderContext* c : v)
+        if (c->pendingBatch) {
+            NR_CHECK(hipSetDevice(c->device));
+            nr_settle(c);
+        }
+}
+
 static int current_device() {
     int d = 0;
     NR_CHECK(hipGetDevice(&d));
@@ -182,6 +199,7 @@ void nr_ensure_depth(RenderContext* ctx) {
 }
 
 void nr_materialize_color(RenderContext* ctx) {
+    nr_settle(ctx);
     if (!ctx->pendColor) return;
     ctx->pendColor = false;
     ctx->frameU8Valid = false;
@@ -193,6 +211,7 @@ void nr_materialize_color(RenderContext* ctx) {
 }
 
 void nr_materialize_depth(RenderContext* ctx) {
+    nr_settle(ctx);
     if (!ctx->pendDepth) return;
     ctx->pendDepth = false;
     nr_ensure_depth(ctx);
@@ -282,6 +301,10 @@ RenderContext* CreateRenderContext(i64 width, i64 height, bool enableAlpha) {
     }
     // The reference leaves the buffer uninitialised (A.11); zero it once.
     NR_CHECK(hipMemsetAsync(ctx->buffer, 0, (size_t)(n > 0 ? n : 1) * sizeof(f64), ctx->stream));
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        g_ctxs.push_back(ctx);
+    }
     return ctx;
 }
 
@@ -289,6 +312,12 @@ RenderContext* CreateRenderContext(i64 width, i64 height, bool enableAlpha) {
 void DestroyRenderContext(RenderContext* ctx) {
     if (!ctx) return;
     NR_CHECK(hipSetDevice(ctx->device));
+    nr_settle(ctx);
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        for (size_t i = 0; i < g_ctxs.size(); ++i)
+            if (g_ctxs[i] == ctx) { g_ctxs.erase(g_ctxs.begin() + i); break; }
+    }
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
@@ -297,6 +326,8 @@ void DestroyRenderContext(RenderContext* ctx) {
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));
+    if (t.h_plan) NR_CHECK(hipHostFree(t.h_plan));
+    if (t.planEvent) NR_CHECK(hipEventDestroy(t.planEvent));
     for (auto& p : ctx->evPending) {
         NR_CHECK(hipEventDestroy(p.second.first));
         NR_CHECK(hipEventDestroy(p.second.second));
@@ -309,6 +340,7 @@ void DestroyRenderContext(RenderContext* ctx) {
 void ResizeRenderContext(RenderContext* ctx, i64 width, i64 height) {
     ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
+    nr_settle(ctx);
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     NR_CHECK(hipFree(ctx->buffer));
     if (ctx->depth) NR_CHECK(hipFree(ctx->depth));
@@ -574,6 +606,7 @@ bool ApplyPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
 void SetColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
     ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
+    nr_settle(ctx);
     if (r == g && g == b && b == a) {
         // uniform clear: kept pending, consumed on chip by the tiled raster
         ctx->pendColor = true;
@@ -641,6 +674,7 @@ i64 GetContextDevice(RenderContext* ctx) { return ctx->device; }
 // Blocks until every queued draw of the context has finished.
 void Flush(RenderContext* ctx) {
     NR_CHECK(hipSetDevice(ctx->device));
+    nr_settle(ctx);
     NR_CHECK(hipStreamSynchronize(ctx->stream));
 }
 

@@ -48,6 +48,10 @@ struct TriScratch {
     u32* flist = nullptr; size_t flist_cap = 0;
     u64* vis = nullptr; size_t vis_cap = 0;
     u32* dplan = nullptr;
+    u32* h_plan = nullptr;                  // pinned copy of the plan totals
+    hipEvent_t planEvent = nullptr;
+    u64 lastPairs = 0;                      // capacity estimate for the next batch
+    u64 capOverride = 0;                    // testing: force this pair capacity
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
 };
 
@@ -91,6 +95,7 @@ struct RenderContext {
     iu8* frameU8 = nullptr; size_t frameU8cap = 0;   // assembled u8 frame (GatherFrameU8)
     bool frameOutput = false;   // set by GatherFrameU8: resolves also write the u8 frame
     bool frameU8Valid = false;  // frameU8 holds the u8 image of every owned pixel
+    void* pendingBatch = nullptr;   // last visibility batch awaiting validation (nr_settle)
 };
 
 struct Texture {
@@ -122,6 +127,8 @@ void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
 void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);
 void nr_fill_f64(hipStream_t s, f64* p, i64 n, f64 v);
 void nr_fill_u32(hipStream_t s, u32* p, i64 n, u32 v);
+void nr_settle(RenderContext* ctx);               // validate an asynchronously sized batch
+void nr_settle_all();                             // ... of every live context
 
 // x86-64 cvttsd2si semantics for (i64)double: out of range / NaN -> INT64_MIN
 static inline i64 nr_f2i64(f64 v) {

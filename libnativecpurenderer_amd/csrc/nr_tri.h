@@ -156,5 +156,6 @@ void finish_batch(RenderContext* ctx, const FrameParams& fp);
 // the two rasterisers (host side)
 void draw_ordered(RenderContext* ctx, const TriSrc& src);
 void draw_free(RenderContext* ctx, const TriSrc& src);
+void settle(RenderContext* ctx);
 
 }  // namespace nrtri

@@ -116,6 +116,7 @@ Opacity device_opacity(RenderContext* ctx, const TriSrc& src) {
 
 void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud, Opacity opq) {
     NR_CHECK(hipSetDevice(ctx->device));
+    settle(ctx);
     if (n <= 0 || ctx->width <= 0 || ctx->height <= 0) return;
     if (!ctx->depthTest) nr_materialize_depth(ctx);
     TriSrc src{xy, z, rgba, gouraud ? 1 : 0, n};
@@ -129,6 +130,8 @@ void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 
 }  // namespace nrtri
 
 using namespace nrtri;
+
+void nr_settle(RenderContext* ctx) { nrtri::settle(ctx); }
 
 extern "C" {
 
@@ -147,6 +150,7 @@ void ClearDepth(RenderContext* ctx, u32 value) {
 // New: copy the W*H u32 depth buffer to the host.
 void GetDepthBuffer(RenderContext* ctx, u32* out) {
     NR_CHECK(hipSetDevice(ctx->device));
+    settle(ctx);
     nr_ensure_depth(ctx);
     nr_materialize_depth(ctx);
     NR_CHECK(hipMemcpyAsync(out, ctx->depth, (size_t)(ctx->width * ctx->height) * sizeof(u32), hipMemcpyDeviceToHost,
@@ -163,6 +167,7 @@ void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const 
 // New: triangles from host arrays (copied to HBM first).
 void DrawTriangles(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud) {
     NR_CHECK(hipSetDevice(ctx->device));
+    settle(ctx);   // a pending batch may still read the staging buffer
     if (n <= 0) return;
     const size_t ncol = gouraud ? 12 : 4;
     const size_t need = (size_t)n * (6 + 3 + ncol);
@@ -204,6 +209,9 @@ TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f
 
 void DestroyTriangleBuffer(TriangleBuffer* tb) {
     if (!tb) return;
+    // a context's pending batch may reference tb: the stream sync below
+    // completes it; an overflow re-run would need tb, so settle all first
+    nr_settle_all();
     NR_CHECK(hipSetDevice(tb->device));
     NR_CHECK(hipStreamSynchronize(nr_stream_for(tb->device)));
     if (tb->xy) NR_CHECK(hipFree(tb->xy));
@@ -229,6 +237,10 @@ i64 GetFragmentCount(RenderContext* ctx) { return (i64)ctx->fragTotal; }
 
 // New: which raster the last batch took (1 = order-free, 2 = ordered).
 i64 GetLastRasterPath(RenderContext* ctx) { return ctx->lastPath; }
+
+// New (testing): cap the visibility path's pair list (0 = automatic), to
+// exercise the overflow re-run of nr_settle.
+void SetPairCapacityOverride(RenderContext* ctx, i64 pairs) { ctx->tri.capOverride = (u64)(pairs > 0 ? pairs : 0); }
 
 // New (testing / A-B measurement): force the ordered raster for every batch.
 void SetForceOrderedRaster(RenderContext* ctx, bool on) { ctx->forceOrdered = on ? 1 : 0; }

@@ -73,8 +73,11 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
 // Single workgroup: off[i] = sum(cnt[<i]), soff[i] = sum(ceil(cnt[<i]/SLICE)),
 // off[ntiles] = P, soff[ntiles] = number of work items; totals = {P, items,
 // number of tiles split over more than one slice}.
+// totals[3] = 1 when the pair list fits `cap`; every later kernel of the
+// batch reads it and does nothing otherwise (the host then re-runs the batch
+// with an exact allocation before anything else is enqueued, nr_settle).
 __global__ __launch_bounds__(1024) void k_free_plan(const u32* __restrict__ cnt, int ntiles, u32* __restrict__ off,
-                                                    u32* __restrict__ soff, u32* __restrict__ totals) {
+                                                    u32* __restrict__ soff, u32* __restrict__ totals, u32 cap) {
     __shared__ u32 sA[1024], sB[1024], sC[1024];
     const int tid = threadIdx.x;
     const int per = (ntiles + 1023) / 1024;
@@ -110,13 +113,16 @@ __global__ __launch_bounds__(1024) void k_free_plan(const u32* __restrict__ cnt,
         totals[0] = sA[1023];
         totals[1] = sB[1023];
         totals[2] = sC[1023];
+        totals[3] = sA[1023] <= cap ? 1u : 0u;
     }
 }
 
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32* __restrict__ off,
-                                                   u32* __restrict__ cur, u32* __restrict__ list, int ntiles) {
+                                                   u32* __restrict__ cur, u32* __restrict__ list, int ntiles,
+                                                   const u32* __restrict__ plan) {
     extern __shared__ u32 hist[];
+    if (!plan[3]) return;
     const int tid = threadIdx.x;
     const i64 base = (i64)blockIdx.x * 256 * TPT;
     if (LDSH) {
@@ -163,7 +169,8 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 // slices merge with global atomics).
 template <int ZMODE>
 __global__ __launch_bounds__(256) void k_vis_init_multi(const FrameParams fp, const u32* __restrict__ off,
-                                                        u64* __restrict__ vis) {
+                                                        u64* __restrict__ vis, const u32* __restrict__ plan) {
+    if (!plan[3]) return;
     const int tile = blockIdx.x;
     if (off[tile + 1] - off[tile] <= SLICE) return;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
@@ -184,7 +191,7 @@ enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_E1X, F_E1Y, F_E2X, F_E2Y, F_INV
 template <int ZMODE, bool COUNT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __restrict__ off,
                                              const u32* __restrict__ soff, const u32* __restrict__ list,
-                                             u64* __restrict__ vis) {
+                                             u64* __restrict__ vis, const u32* __restrict__ plan) {
     constexpr bool DEPTH = ZMODE != 0;
     __shared__ u64 key[TH * TW];
     __shared__ u32 zin[ZMODE == 2 ? TH * TW : 1];
@@ -194,9 +201,16 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     __shared__ iu8 RR0[FCH];
     __shared__ int sTile;
     __shared__ unsigned long long sFrag;
+    if (!plan[3]) return;
     const int tid = threadIdx.x;
     const int ntiles = fp.tiles_x * fp.tiles_y;
-    const u32 item = blockIdx.x;
+    const u32 nitems = plan[1];
+    unsigned long long myFrags = 0;
+    if (COUNT && tid == 0) sFrag = 0;
+    // grid-stride over the work items (the grid is sized from a capacity
+    // bound, not from the item count, so no host sync is needed)
+    for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {
+    __syncthreads();
     if (tid == 0) {   // tile of this work item: last tile with soff[tile] <= item
         int lo = 0, hi = ntiles;
         while (hi - lo > 1) {
@@ -204,7 +218,6 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             if (soff[mid] <= item) lo = mid; else hi = mid;
         }
         sTile = lo;
-        sFrag = 0;
     }
     __syncthreads();
     const int tile = sTile;
@@ -226,7 +239,6 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
         key[p] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
         if (ZMODE == 2) zin[p] = z0;
     }
-    unsigned long long myFrags = 0;
 
     // next chunk's triangle, prefetched into registers during phase (c)
     u32 pt = 0;
@@ -355,7 +367,9 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
         else if (ZMODE == 1) atomicMin(g, key[p]);
         else atomicMax(g, key[p]);
     }
+    }   // work items
     if (COUNT) {
+        __syncthreads();
         atomicAdd(&sFrag, myFrags);
         __syncthreads();
         if (tid == 0) atomicAdd(fp.fragCounter, sFrag);
@@ -365,7 +379,8 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
 // One thread per pixel (2-D grid: x blocks of 256, one row per blockIdx.y).
 template <int ZMODE, bool GOURAUD>
 __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32* __restrict__ off,
-                                                 const u64* __restrict__ vis) {
+                                                 const u64* __restrict__ vis, const u32* __restrict__ plan) {
+    if (!plan[3]) return;
     const i64 px = (i64)blockIdx.x * 256 + threadIdx.x;
     // blockIdx.y enumerates the rows of the owned tile rows only
     const i64 py = ((i64)(blockIdx.y / TH) * fp.nshards + fp.shard) * TH + blockIdx.y % TH;
@@ -449,46 +464,58 @@ __global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32
 }
 
 template <int Z, bool C>
-void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u32* list, u64* vis, u32 items,
-                hipStream_t s) {
-    hipLaunchKernelGGL((k_vis<Z, C>), dim3(items), dim3(VWG), 0, s, fp, off, soff, list, vis);
+void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u32* list, u64* vis, u32 grid,
+                const u32* plan, hipStream_t s) {
+    hipLaunchKernelGGL((k_vis<Z, C>), dim3(grid), dim3(VWG), 0, s, fp, off, soff, list, vis, plan);
 }
 
 template <int Z, bool G>
-void launch_resolve(const FrameParams& fp, const u32* off, const u64* vis, hipStream_t s) {
+void launch_resolve(const FrameParams& fp, const u32* off, const u64* vis, const u32* plan, hipStream_t s) {
     const int owned = (fp.tiles_y - fp.shard + fp.nshards - 1) / fp.nshards;
     if (owned <= 0) return;
     dim3 grid((unsigned)((fp.W + 255) / 256), (unsigned)(owned * TH));
-    hipLaunchKernelGGL((k_resolve<Z, G>), grid, dim3(256), 0, s, fp, off, vis);
+    hipLaunchKernelGGL((k_resolve<Z, G>), grid, dim3(256), 0, s, fp, off, vis, plan);
 }
 
-}  // namespace
+// Everything a batch needs to be re-run after an overflow (nr_settle).
+struct PendingBatch {
+    TriSrc src;
+    FrameParams fp;
+    BinParams bp;
+};
 
-void draw_free(RenderContext* ctx, const TriSrc& src) {
+// Enqueues one batch.  exact: read the pair/item totals back (host sync) and
+// allocate exactly; otherwise size the list from `cap`, let the plan kernel
+// check it on the device and validate later (nr_settle).
+static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
+                         bool exact) {
     hipStream_t s = ctx->stream;
     TriScratch& sc = ctx->tri;
-    FrameParams fp = frame_params(ctx, src);
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
     const bool g = src.gouraud != 0;
-    if (ctx->frameOutput && fp.pendColor) {
-        const size_t n = (size_t)(ctx->width * ctx->height * fp.ipp);
-        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
-    }
-
-    BinParams bp;
-    bp.src = src;
-    for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
-    bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
-    bp.nshards = fp.nshards; bp.shard = fp.shard;
 
     u32* tb[4] = {sc.fcnt, sc.foff, sc.fsoff, sc.fcur};
-    if (!grow_set(tb, &sc.ftile_cap, (size_t)ntiles + 1)) return;
+    if (!grow_set(tb, &sc.ftile_cap, (size_t)ntiles + 1)) return false;
     sc.fcnt = tb[0]; sc.foff = tb[1]; sc.fsoff = tb[2]; sc.fcur = tb[3];
     if (!sc.dplan) NR_CHECK(hipMalloc(&sc.dplan, 4 * sizeof(u32)));
+    if (!sc.h_plan) NR_CHECK(hipHostMalloc((void**)&sc.h_plan, 4 * sizeof(u32)));
+    u64* vb[1] = {sc.vis};
+    if (!grow_set(vb, &sc.vis_cap, (size_t)(ctx->width * ctx->height))) return false;
+    sc.vis = vb[0];
+
+    size_t cap = 0xFFFFFFFFull;
+    if (!exact) {
+        const u64 est = std::max<u64>(std::max<u64>(sc.lastPairs + sc.lastPairs / 4, (u64)src.n * 2), 1u << 20);
+        cap = (size_t)std::min<u64>(sc.capOverride ? sc.capOverride : est, 0xFFFFFFF0ull);
+        u32* lb[1] = {sc.flist};
+        if (!grow_set(lb, &sc.flist_cap, cap)) return false;
+        sc.flist = lb[0];
+        if (!sc.capOverride) cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
+    }
+
     NR_CHECK(hipMemsetAsync(sc.fcnt, 0, (size_t)ntiles * sizeof(u32), s));
     NR_CHECK(hipMemsetAsync(sc.fcur, 0, (size_t)ntiles * sizeof(u32), s));
-
     const bool ldsh = ntiles <= LDS_HIST_MAX;
     const size_t hbytes = ldsh ? (size_t)ntiles * sizeof(u32) : 0;
     const int gb = (int)((src.n + 256 * TPT - 1) / (256 * TPT));
@@ -500,58 +527,105 @@ void draw_free(RenderContext* ctx, const TriSrc& src) {
     nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
 
     nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
-    hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, sc.foff, sc.fsoff, sc.dplan);
+    hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, sc.foff, sc.fsoff, sc.dplan, (u32)cap);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
+    NR_CHECK(hipMemcpyAsync(sc.h_plan, sc.dplan, 4 * sizeof(u32), hipMemcpyDeviceToHost, s));
 
-    // pair and work-item totals: size the list and the k_vis grid (host sync)
-    u32* hp = reinterpret_cast<u32*>(sc.h_total);
-    NR_CHECK(hipMemcpyAsync(hp, sc.dplan, 3 * sizeof(u32), hipMemcpyDeviceToHost, s));
-    NR_CHECK(hipStreamSynchronize(s));
-    const u32 P = hp[0], items = hp[1], multi = hp[2];
-
-    if (P > 0) {
+    u32 grid;
+    bool multi = true;
+    if (exact) {
+        NR_CHECK(hipStreamSynchronize(s));
+        const u32 P = sc.h_plan[0];
+        grid = sc.h_plan[1];
+        multi = sc.h_plan[2] != 0;
+        sc.lastPairs = P;
         u32* lb[1] = {sc.flist};
-        if (!grow_set(lb, &sc.flist_cap, (size_t)P)) return;
+        if (!grow_set(lb, &sc.flist_cap, (size_t)std::max<u32>(P, 1))) return false;
         sc.flist = lb[0];
-        u64* vb[1] = {sc.vis};
-        if (!grow_set(vb, &sc.vis_cap, (size_t)(ctx->width * ctx->height))) return;
-        sc.vis = vb[0];
+    } else {
+        if (!sc.planEvent) NR_CHECK(hipEventCreateWithFlags(&sc.planEvent, hipEventDisableTiming));
+        NR_CHECK(hipEventRecord(sc.planEvent, s));
+        // a bound on the work items: every non-empty tile + one per full slice
+        const u64 bound = (u64)ntiles + cap / SLICE + 1;
+        grid = (u32)std::min<u64>(bound, 8192);
+    }
 
-        nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
-        if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, sc.flist, ntiles);
-        else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, sc.flist, ntiles);
+    nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
+    if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.dplan);
+    else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.dplan);
+    NR_CHECK(hipGetLastError());
+    nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
+
+    if (multi) {
+        nr_timing_begin(ctx, NRK_VIS_INIT, &e0, &e1);
+        if (zmode == 1) hipLaunchKernelGGL(k_vis_init_multi<1>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis, sc.dplan);
+        else hipLaunchKernelGGL(k_vis_init_multi<0>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis, sc.dplan);
         NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
+        nr_timing_end(ctx, NRK_VIS_INIT, e0, e1);
+    }
 
-        if (multi) {
-            nr_timing_begin(ctx, NRK_VIS_INIT, &e0, &e1);
-            if (zmode == 1) hipLaunchKernelGGL(k_vis_init_multi<1>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis);
-            else hipLaunchKernelGGL(k_vis_init_multi<0>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis);
-            NR_CHECK(hipGetLastError());
-            nr_timing_end(ctx, NRK_VIS_INIT, e0, e1);
-        }
-
+    if (grid > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool C = fp.fragCounter != nullptr;
-        if (zmode == 1) { if (C) launch_vis<1, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<1, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
-        else if (zmode == 2) { if (C) launch_vis<2, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<2, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
-        else { if (C) launch_vis<0, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); else launch_vis<0, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, items, s); }
+        if (zmode == 1) { if (C) launch_vis<1, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); else launch_vis<1, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); }
+        else if (zmode == 2) { if (C) launch_vis<2, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); else launch_vis<2, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); }
+        else { if (C) launch_vis<0, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); else launch_vis<0, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
     }
 
-    if (P > 0 || fp.pendColor || (zmode != 0 && fp.pendDepth)) {
-        nr_timing_begin(ctx, NRK_RESOLVE, &e0, &e1);
-        const u64* vis = sc.vis ? sc.vis : reinterpret_cast<const u64*>(sc.foff);   // unread when P == 0
-        if (zmode == 1) { if (g) launch_resolve<1, true>(fp, sc.foff, vis, s); else launch_resolve<1, false>(fp, sc.foff, vis, s); }
-        else if (zmode == 2) { if (g) launch_resolve<2, true>(fp, sc.foff, vis, s); else launch_resolve<2, false>(fp, sc.foff, vis, s); }
-        else { if (g) launch_resolve<0, true>(fp, sc.foff, vis, s); else launch_resolve<0, false>(fp, sc.foff, vis, s); }
-        NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_RESOLVE, e0, e1);
+    nr_timing_begin(ctx, NRK_RESOLVE, &e0, &e1);
+    if (zmode == 1) { if (g) launch_resolve<1, true>(fp, sc.foff, sc.vis, sc.dplan, s); else launch_resolve<1, false>(fp, sc.foff, sc.vis, sc.dplan, s); }
+    else if (zmode == 2) { if (g) launch_resolve<2, true>(fp, sc.foff, sc.vis, sc.dplan, s); else launch_resolve<2, false>(fp, sc.foff, sc.vis, sc.dplan, s); }
+    else { if (g) launch_resolve<0, true>(fp, sc.foff, sc.vis, sc.dplan, s); else launch_resolve<0, false>(fp, sc.foff, sc.vis, sc.dplan, s); }
+    NR_CHECK(hipGetLastError());
+    nr_timing_end(ctx, NRK_RESOLVE, e0, e1);
+    return true;
+}
+
+}  // namespace
+
+void draw_free(RenderContext* ctx, const TriSrc& src) {
+    FrameParams fp = frame_params(ctx, src);
+    if (ctx->frameOutput && fp.pendColor) {
+        const size_t n = (size_t)(ctx->width * ctx->height * fp.ipp);
+        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
+    }
+    BinParams bp;
+    bp.src = src;
+    for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
+    bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
+    bp.nshards = fp.nshards; bp.shard = fp.shard;
+    // fragment counting reads a counter back anyway: run exact (synchronous)
+    const bool exact = fp.fragCounter != nullptr;
+    if (!free_enqueue(ctx, src, fp, bp, exact)) return;
+    if (!exact) {
+        PendingBatch* pb = new PendingBatch{src, fp, bp};
+        ctx->pendingBatch = pb;
     }
     ctx->lastPath = 1;
     finish_batch(ctx, fp);
+}
+
+// Validates the last asynchronously sized batch of `ctx`: waits for its plan
+// kernel (usually long finished), and if the pair list did not fit, re-runs
+// the batch with an exact allocation.  Called at the start of every API
+// entry point that enqueues work on, or reads, the context's buffers, so the
+// re-run is ordered before anything that depends on the batch.
+void settle(RenderContext* ctx) {
+    PendingBatch* pb = reinterpret_cast<PendingBatch*>(ctx->pendingBatch);
+    if (!pb) return;
+    ctx->pendingBatch = nullptr;
+    TriScratch& sc = ctx->tri;
+    NR_CHECK(hipEventSynchronize(sc.planEvent));
+    if (sc.h_plan[3]) {
+        sc.lastPairs = sc.h_plan[0];
+    } else {
+        sc.lastPairs = sc.h_plan[0];
+        free_enqueue(ctx, pb->src, pb->fp, pb->bp, true);   // context flags were applied at the first launch
+    }
+    delete pb;
 }
 
 }  // namespace nrtri

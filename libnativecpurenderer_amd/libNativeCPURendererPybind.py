@@ -313,6 +313,10 @@ class RenderContext:
     def set_force_ordered_raster(self, on: bool = True):
         lib.SetForceOrderedRaster(self._ptr, on)
 
+    def set_pair_capacity_override(self, pairs: int):
+        """Testing: cap the visibility raster's (tile, triangle) list (0 = auto)."""
+        lib.SetPairCapacityOverride(self._ptr, pairs)
+
 
 class Texture:
     """Texels in HBM as f64, same interleaved layout as the framebuffer

@@ -242,3 +242,27 @@ def test_fused_frame_output_matches_conversion(gpu):
             ctx.draw_rect(20, 20, 50, 40, 1, 0, 0, 0.5)
         ctx.gather_frame_u8()
         assert np.array_equal(ctx.get_frame_u8(), ctx.get_buffer_as_uint8_numpy()), frame
+
+
+def test_pair_list_overflow_is_rerun_in_order(gpu, oracle):
+    """The visibility raster sizes its pair list from an estimate and checks it
+    on the device; an overflowing batch does nothing and is re-run, before any
+    later call, with an exact allocation.  Force that with a tiny capacity and
+    interleave other operations: the frame must still equal the oracle's."""
+    W, H = 260, 190
+    xy, z, c = scenes.triangle_soup(1500, W, H, 25, seed=61, gouraud=True)
+    outs = []
+    for fac in (gpu, oracle):
+        ctx = fac.context(W, H, True)
+        if fac is gpu:
+            ctx.set_pair_capacity_override(50)
+        ctx.set_color(0.2, 0.2, 0.2, 0.2)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.draw_triangles(xy, c, z=z)                   # overflows -> re-run at the next call
+        ctx.draw_rect(30, 30, 80, 60, 0.9, 0.1, 0.1, 0.5)
+        ctx.set_color(0.4, 0.4, 0.4, 0.4)                # pending clear after an overflowed batch
+        ctx.draw_triangles(xy[::-1], c[::-1], z=z[::-1])
+        ctx.draw_triangles(xy[:200] + 3.5, c[:200], z=z[:200])
+        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+    assert_same(outs[0], outs[1], "overflow")
