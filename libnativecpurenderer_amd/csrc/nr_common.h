@@ -48,7 +48,8 @@ struct TriScratch {
     u32* flist = nullptr; size_t flist_cap = 0;
     u64* vis = nullptr; size_t vis_cap = 0;
     u32* dplan = nullptr;
-    u32* h_plan = nullptr;                  // pinned copy of the plan totals
+    u32* h_plan = nullptr;                  // pinned, device-mapped copy of the plan totals
+    u32* d_hplan = nullptr;                 // its device address
     hipEvent_t planEvent = nullptr;
     u64 lastPairs = 0;                      // capacity estimate for the next batch
     u64 capOverride = 0;                    // testing: force this pair capacity

@@ -76,8 +76,12 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
 // totals[3] = 1 when the pair list fits `cap`; every later kernel of the
 // batch reads it and does nothing otherwise (the host then re-runs the batch
 // with an exact allocation before anything else is enqueued, nr_settle).
-__global__ __launch_bounds__(1024) void k_free_plan(const u32* __restrict__ cnt, int ntiles, u32* __restrict__ off,
-                                                    u32* __restrict__ soff, u32* __restrict__ totals, u32 cap) {
+// It also re-zeroes the tile counters for the next batch (after reading them)
+// and the emit cursors, and mirrors the totals into pinned host memory, so a
+// batch needs no memset and no copy command.
+__global__ __launch_bounds__(1024) void k_free_plan(u32* __restrict__ cnt, int ntiles, u32* __restrict__ off,
+                                                    u32* __restrict__ soff, u32* __restrict__ cur,
+                                                    u32* __restrict__ totals, u32* __restrict__ host_totals, u32 cap) {
     __shared__ u32 sA[1024], sB[1024], sC[1024];
     const int tid = threadIdx.x;
     const int per = (ntiles + 1023) / 1024;
@@ -106,14 +110,17 @@ __global__ __launch_bounds__(1024) void k_free_plan(const u32* __restrict__ cnt,
         soff[i] = eb;
         ea += c;
         eb += (c + SLICE - 1) / SLICE;
+        cnt[i] = 0;
+        cur[i] = 0;
     }
     if (tid == 1023) {
         off[ntiles] = sA[1023];
         soff[ntiles] = sB[1023];
-        totals[0] = sA[1023];
-        totals[1] = sB[1023];
-        totals[2] = sC[1023];
-        totals[3] = sA[1023] <= cap ? 1u : 0u;
+        const u32 t[4] = {sA[1023], sB[1023], sC[1023], sA[1023] <= cap ? 1u : 0u};
+        for (int k = 0; k < 4; ++k) {
+            totals[k] = t[k];
+            __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -496,10 +503,18 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     const bool g = src.gouraud != 0;
 
     u32* tb[4] = {sc.fcnt, sc.foff, sc.fsoff, sc.fcur};
+    const size_t oldcap = sc.ftile_cap;
     if (!grow_set(tb, &sc.ftile_cap, (size_t)ntiles + 1)) return false;
     sc.fcnt = tb[0]; sc.foff = tb[1]; sc.fsoff = tb[2]; sc.fcur = tb[3];
+    if (sc.ftile_cap != oldcap) {   // counters start at zero; k_free_plan re-zeroes them after each use
+        NR_CHECK(hipMemsetAsync(sc.fcnt, 0, sc.ftile_cap * sizeof(u32), s));
+        NR_CHECK(hipMemsetAsync(sc.fcur, 0, sc.ftile_cap * sizeof(u32), s));
+    }
     if (!sc.dplan) NR_CHECK(hipMalloc(&sc.dplan, 4 * sizeof(u32)));
-    if (!sc.h_plan) NR_CHECK(hipHostMalloc((void**)&sc.h_plan, 4 * sizeof(u32)));
+    if (!sc.h_plan) {
+        NR_CHECK(hipHostMalloc((void**)&sc.h_plan, 4 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
+        NR_CHECK(hipHostGetDevicePointer((void**)&sc.d_hplan, sc.h_plan, 0));
+    }
     u64* vb[1] = {sc.vis};
     if (!grow_set(vb, &sc.vis_cap, (size_t)(ctx->width * ctx->height))) return false;
     sc.vis = vb[0];
@@ -514,8 +529,6 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         if (!sc.capOverride) cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
     }
 
-    NR_CHECK(hipMemsetAsync(sc.fcnt, 0, (size_t)ntiles * sizeof(u32), s));
-    NR_CHECK(hipMemsetAsync(sc.fcur, 0, (size_t)ntiles * sizeof(u32), s));
     const bool ldsh = ntiles <= LDS_HIST_MAX;
     const size_t hbytes = ldsh ? (size_t)ntiles * sizeof(u32) : 0;
     const int gb = (int)((src.n + 256 * TPT - 1) / (256 * TPT));
@@ -527,10 +540,10 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
 
     nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
-    hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, sc.foff, sc.fsoff, sc.dplan, (u32)cap);
+    hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, sc.foff, sc.fsoff, sc.fcur, sc.dplan,
+                       sc.d_hplan, (u32)cap);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
-    NR_CHECK(hipMemcpyAsync(sc.h_plan, sc.dplan, 4 * sizeof(u32), hipMemcpyDeviceToHost, s));
 
     u32 grid;
     bool multi = true;
