@@ -132,6 +132,7 @@ void ClearLastError(void);
 void EnableKernelTiming(RenderContext* ctx, bool on);
 bool GetKernelTiming(RenderContext* ctx, const char* name, f64* total_ms, i64* count);
 void ResetKernelTiming(RenderContext* ctx);
+void SetKernelTimingFilter(RenderContext* ctx, const char* names); /* comma-separated kernel names, "" = all */
 
 #ifdef __cplusplus
 }

@@ -101,6 +101,7 @@ DEVICE_ABI = {
     "EnableKernelTiming": (None, (P, B)),
     "GetKernelTiming": (B, (P, ctypes.c_char_p, P, P)),
     "ResetKernelTiming": (None, (P,)),
+    "SetKernelTimingFilter": (None, (P, ctypes.c_char_p)),
 }
 
 HIP_LIBRARY_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **DEVICE_ABI}

@@ -238,9 +238,8 @@ static hipEvent_t ev_get(RenderContext* ctx) {
 }
 
 void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b) {
-    (void)kid;
     *a = *b = nullptr;
-    if (!ctx->timing) return;
+    if (!ctx->timing || !((ctx->timingMask >> kid) & 1ull)) return;
     *a = ev_get(ctx);
     *b = ev_get(ctx);
     NR_CHECK(hipEventRecord(*a, ctx->stream));
@@ -705,6 +704,25 @@ bool GetKernelTiming(RenderContext* ctx, const char* name, f64* total_ms, i64* c
             return true;
         }
     return false;
+}
+
+// Restricts EnableKernelTiming to the named kernels (comma-separated; "" = all).
+void SetKernelTimingFilter(RenderContext* ctx, const char* names) {
+    if (!names || !*names) {
+        ctx->timingMask = ~0ull;
+        return;
+    }
+    ctx->timingMask = 0;
+    std::string all(names);
+    size_t pos = 0;
+    while (pos <= all.size()) {
+        size_t e = all.find(',', pos);
+        if (e == std::string::npos) e = all.size();
+        const std::string n = all.substr(pos, e - pos);
+        for (int k = 0; k < NRK_COUNT_; ++k)
+            if (n == kKernelNames[k]) ctx->timingMask |= 1ull << k;
+        pos = e + 1;
+    }
 }
 
 void ResetKernelTiming(RenderContext* ctx) {

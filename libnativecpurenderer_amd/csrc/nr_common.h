@@ -80,6 +80,7 @@ struct RenderContext {
     TriScratch tri;
     // per-kernel HIP-event timing (bench.py's live roofline measurement)
     bool timing = false;
+    unsigned long long timingMask = ~0ull;   // which NRKernelId are timed
     std::vector<hipEvent_t> evPool;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> evPending;
     f64 kTimeMs[NRK_COUNT_] = {0};

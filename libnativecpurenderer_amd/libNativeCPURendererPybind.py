@@ -271,6 +271,10 @@ class RenderContext:
     def reset_kernel_timing(self):
         lib.ResetKernelTiming(self._ptr)
 
+    def set_kernel_timing_filter(self, names: str = ""):
+        """Time only these kernels (comma-separated names; "" = all)."""
+        lib.SetKernelTimingFilter(self._ptr, names.encode())
+
     def get_kernel_timing(self, name: str):
         """(total_ms, launches) of one kernel since the last reset."""
         tot = ctypes.c_double()
