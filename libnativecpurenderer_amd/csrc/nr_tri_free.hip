@@ -188,13 +188,23 @@ __global__ __launch_bounds__(256) void k_vis_init_multi(const FrameParams fp, co
     }
 }
 
-enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_E1X, F_E1Y, F_E2X, F_E2Y, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
+enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
+constexpr int NW = VWG / 64;   // waves per k_vis workgroup
 
-// Per chunk of FCH triangles: (a) one thread per triangle: setup + the rows
-// of this tile it straddles; (b) exclusive scan of the row counts; (c) the
-// chunk's (triangle, row) items are spread evenly over all threads: one
-// binary search per item, the exact span, then a short per-lane walk over the
-// span's pixels (depth + LDS atomic on the packed key).
+// Wave-synchronous ordering of this wave's own LDS traffic (a wave's LDS
+// operations complete in order; this stops the compiler from reordering them).
+__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+// One workgroup per work item (tile, slice of <= SLICE triangles).  The 4
+// waves share only the tile's 2048 LDS keys; each wave independently walks
+// 64-triangle chunks of the slice (chunk c goes to wave c % 4) with no
+// workgroup barrier:
+//   setup   one lane per triangle: screen vertices, 1/den, depths, the rows of
+//           this tile it straddles (next chunk prefetched into registers)
+//   scan    exclusive scan of the row counts with wave shuffles, then each
+//           lane writes its triangle's lane index into a row->triangle map
+//   rows    the chunk's (triangle, row) items over the 64 lanes: exact span
+//           (row_span), then per pixel depth + LDS atomic on the packed key
 template <int ZMODE, bool COUNT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __restrict__ off,
                                              const u32* __restrict__ soff, const u32* __restrict__ list,
@@ -202,14 +212,15 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     constexpr bool DEPTH = ZMODE != 0;
     __shared__ u64 key[TH * TW];
     __shared__ u32 zin[ZMODE == 2 ? TH * TW : 1];
-    __shared__ f64 S[F_NSLOT][FCH];
-    __shared__ u32 TIDX[FCH];
-    __shared__ u32 ROFF[FCH + 1];
-    __shared__ iu8 RR0[FCH];
+    __shared__ f64 S[NW][F_NSLOT][64];
+    __shared__ iu8 MAP[NW][64 * TH];
+    __shared__ iu8 RR0[NW][64];
+    __shared__ unsigned short ROFF[NW][64];
+    __shared__ u32 TT[NW][64];   // triangle id + 1 of each lane's triangle
     __shared__ int sTile;
     __shared__ unsigned long long sFrag;
     if (!plan[3]) return;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const u32 nitems = plan[1];
     unsigned long long myFrags = 0;
@@ -217,163 +228,144 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     // grid-stride over the work items (the grid is sized from a capacity
     // bound, not from the item count, so no host sync is needed)
     for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {
-    __syncthreads();
-    if (tid == 0) {   // tile of this work item: last tile with soff[tile] <= item
-        int lo = 0, hi = ntiles;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (soff[mid] <= item) lo = mid; else hi = mid;
-        }
-        sTile = lo;
-    }
-    __syncthreads();
-    const int tile = sTile;
-    const u32 t0 = off[tile], t1 = off[tile + 1];
-    const u32 slice = item - soff[tile];
-    const u32 ls = t0 + slice * SLICE;
-    const u32 le = ls + SLICE < t1 ? ls + SLICE : t1;
-    const bool multi = t1 - t0 > SLICE;
-    const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
-    const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
-    const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
-    const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
-
-    for (int p = tid; p < TH * TW; p += VWG) {
-        const int lx = p & (TW - 1), ly = p / TW;
-        u32 z0 = 0xFFFFFFFFu;
-        if (DEPTH && lx < wlim && ly < hlim)
-            z0 = fp.pendDepth ? fp.pendDepthValue : fp.depth[(y0 + ly) * fp.W + x0 + lx];
-        key[p] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
-        if (ZMODE == 2) zin[p] = z0;
-    }
-
-    // next chunk's triangle, prefetched into registers during phase (c)
-    u32 pt = 0;
-    f64 pxy[6], pz[3] = {0, 0, 0};
-    auto prefetch = [&](u32 b) {
-        if (b + tid < le && tid < FCH) {
-            pt = list[b + tid];
-            const f64* q = fp.src.xy + (i64)pt * 6;
-#pragma unroll
-            for (int v = 0; v < 6; ++v) pxy[v] = q[v];
-            if (DEPTH && fp.src.z) {
-                const f64* qz = fp.src.z + (i64)pt * 3;
-                pz[0] = qz[0]; pz[1] = qz[1]; pz[2] = qz[2];
-            }
-        }
-    };
-    prefetch(ls);
-
-    for (u32 base = ls; base < le; base += FCH) {
-        const int cnt = (le - base) < (u32)FCH ? (int)(le - base) : FCH;
         __syncthreads();
-        // ---- (a) setup, one thread per triangle
-        if (tid < cnt) {
-            const u32 t = pt;
-            f64 sx[3], sy[3];
-#pragma unroll
-            for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
-            const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-            const f64 den = e1x * e2y - e2x * e1y;
-            const bool ok = tri_finite(sx, sy) && den != 0;
-            S[F_X0][tid] = sx[0]; S[F_Y0][tid] = sy[0];
-            S[F_X1][tid] = sx[1]; S[F_Y1][tid] = sy[1];
-            S[F_X2][tid] = sx[2]; S[F_Y2][tid] = sy[2];
-            S[F_E1X][tid] = e1x; S[F_E1Y][tid] = e1y; S[F_E2X][tid] = e2x; S[F_E2Y][tid] = e2y;
-            S[F_INV][tid] = 1.0 / den;
-            if (DEPTH) {
-                S[F_Z0][tid] = pz[0]; S[F_DZ1][tid] = pz[1] - pz[0]; S[F_DZ2][tid] = pz[2] - pz[0];
-            }
-            TIDX[tid] = t;
-            int r0 = 0, nr = 0;
-            if (ok) {
-                // rows with a straddling edge: ymin <= y < ymax (exact)
-                const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
-                r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
-                const int r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
-                nr = r1 > r0 ? r1 - r0 : 0;
-            }
-            RR0[tid] = (iu8)r0;
-            ROFF[tid] = (u32)nr;
-        }
-        __syncthreads();
-        prefetch(base + FCH);
-        // ---- (b) exclusive scan of the row counts (wave 0)
-        if (tid < 64) {
-            constexpr int PER = FCH / 64;
-            u32 v[PER];
-            u32 sum = 0;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int idx = tid * PER + i;
-                v[i] = idx < cnt ? ROFF[idx] : 0u;
-                sum += v[i];
-            }
-            u32 incl = sum;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const u32 o = __shfl_up(incl, d, 64);
-                if (tid >= d) incl += o;
-            }
-            u32 ex = incl - sum;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                ROFF[tid * PER + i] = ex;
-                ex += v[i];
-            }
-            if (tid == 63) ROFF[FCH] = incl;
-        }
-        __syncthreads();
-        // ---- (c) (triangle, row) items over all threads
-        const u32 R = ROFF[cnt];
-#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-        for (u32 it = tid; it < R; it += VWG) {
-            int lo = 0, hi = cnt;   // ROFF[lo] <= it < ROFF[hi]
+        if (tid == 0) {   // tile of this work item: last tile with soff[tile] <= item
+            int lo = 0, hi = ntiles;
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
-                if (ROFF[mid] <= it) lo = mid; else hi = mid;
+                if (soff[mid] <= item) lo = mid; else hi = mid;
             }
-            const int k = lo;
-            const int r = RR0[k] + (int)(it - ROFF[k]);
-            const f64 sx[3] = {S[F_X0][k], S[F_X1][k], S[F_X2][k]};
-            const f64 sy[3] = {S[F_Y0][k], S[F_Y1][k], S[F_Y2][k]};
-            const f64 y = (f64)(y0 + r);
-            int xs, xe;
-            row_span(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);
-            if (COUNT) myFrags += (unsigned long long)(xe - xs);
-            if (xs >= xe) continue;
-            const u64 id1 = (u64)TIDX[k] + 1;
-            if (ZMODE == 0) {
-#pragma clang loop vectorize(disable) interleave(disable)
-                for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * TW + lx], id1);
-                continue;
-            }
-            const f64 e1x = S[F_E1X][k], e1y = S[F_E1Y][k], e2x = S[F_E2X][k], e2y = S[F_E2Y][k];
-            const f64 inv = S[F_INV][k];
-            const f64 zz0 = S[F_Z0][k], dz1 = S[F_DZ1][k], dz2 = S[F_DZ2][k];
-            const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
-#pragma clang loop vectorize(disable) interleave(disable)
-            for (int lx = xs; lx < xe; ++lx) {
-                const f64 dx = (f64)(x0 + lx) - sx[0];
-                const f64 w1 = (dx * e2y - e2x * dy) * inv;
-                const f64 w2 = (e1x * dy - dx * e1y) * inv;
-                const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
-                const u32 zq = nr_quantize_depth(zz);
-                const int p = r * TW + lx;
-                if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
-                else if (zq < zin[p]) atomicMax(&key[p], id1);
-            }
+            sTile = lo;
         }
-    }
-    __syncthreads();
-    for (int p = tid; p < TH * TW; p += VWG) {
-        const int lx = p & (TW - 1), ly = p / TW;
-        if (lx >= wlim || ly >= hlim) continue;
-        u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-        if (!multi) *g = key[p];
-        else if (ZMODE == 1) atomicMin(g, key[p]);
-        else atomicMax(g, key[p]);
-    }
+        __syncthreads();
+        const int tile = sTile;
+        const u32 t0 = off[tile], t1 = off[tile + 1];
+        const u32 slice = item - soff[tile];
+        const u32 ls = t0 + slice * SLICE;
+        const u32 le = ls + SLICE < t1 ? ls + SLICE : t1;
+        const bool multi = t1 - t0 > SLICE;
+        const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
+        const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
+        const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
+        const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
+
+        for (int p = tid; p < TH * TW; p += VWG) {
+            const int lx = p & (TW - 1), ly = p / TW;
+            u32 z0 = 0xFFFFFFFFu;
+            if (DEPTH && lx < wlim && ly < hlim)
+                z0 = fp.pendDepth ? fp.pendDepthValue : fp.depth[(y0 + ly) * fp.W + x0 + lx];
+            key[p] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
+            if (ZMODE == 2) zin[p] = z0;
+        }
+        __syncthreads();
+
+        // this wave's chunks: c = wave, wave + NW, ...
+        const u32 nch = (le - ls + 63) / 64;
+        u32 pt = 0;
+        f64 pxy[6], pz[3] = {0, 0, 0};
+        auto prefetch = [&](u32 c) {
+            const u32 b = ls + c * 64 + lane;
+            if (c < nch && b < le) {
+                pt = list[b];
+                const f64* q = fp.src.xy + (i64)pt * 6;
+#pragma unroll
+                for (int v = 0; v < 6; ++v) pxy[v] = q[v];
+                if (DEPTH && fp.src.z) {
+                    const f64* qz = fp.src.z + (i64)pt * 3;
+                    pz[0] = qz[0]; pz[1] = qz[1]; pz[2] = qz[2];
+                }
+            }
+        };
+        prefetch(wave);
+        for (u32 c = wave; c < nch; c += NW) {
+            const u32 base = ls + c * 64;
+            const int cnt = (le - base) < 64u ? (int)(le - base) : 64;
+            // ---- setup (lane = triangle)
+            const u32 t = pt;
+            int r0 = 0, nr = 0;
+            if (lane < cnt) {
+                f64 sx[3], sy[3];
+#pragma unroll
+                for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
+                const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+                const f64 den = e1x * e2y - e2x * e1y;
+                const bool ok = tri_finite(sx, sy) && den != 0;
+                S[wave][F_X0][lane] = sx[0]; S[wave][F_Y0][lane] = sy[0];
+                S[wave][F_X1][lane] = sx[1]; S[wave][F_Y1][lane] = sy[1];
+                S[wave][F_X2][lane] = sx[2]; S[wave][F_Y2][lane] = sy[2];
+                S[wave][F_INV][lane] = 1.0 / den;
+                if (DEPTH) {
+                    S[wave][F_Z0][lane] = pz[0]; S[wave][F_DZ1][lane] = pz[1] - pz[0];
+                    S[wave][F_DZ2][lane] = pz[2] - pz[0];
+                }
+                if (ok) {
+                    // rows with a straddling edge: ymin <= y < ymax (exact)
+                    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+                    r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
+                    const int r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
+                    nr = r1 > r0 ? r1 - r0 : 0;
+                }
+            }
+            prefetch(c + NW);
+            // ---- scan of the row counts, row -> triangle map
+            int incl = nr;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int o = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += o;
+            }
+            const int ex = incl - nr;
+            const int R = __shfl(incl, 63, 64);
+            TT[wave][lane] = t + 1;
+            RR0[wave][lane] = (iu8)r0;
+            ROFF[wave][lane] = (unsigned short)ex;
+            for (int j = 0; j < nr; ++j) MAP[wave][ex + j] = (iu8)lane;
+            wave_lds_fence();
+            // ---- (triangle, row) items over the lanes
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+            for (int it = lane; it < R; it += 64) {
+                const int k = MAP[wave][it];
+                const int r = RR0[wave][k] + (it - ROFF[wave][k]);
+                const f64 sx[3] = {S[wave][F_X0][k], S[wave][F_X1][k], S[wave][F_X2][k]};
+                const f64 sy[3] = {S[wave][F_Y0][k], S[wave][F_Y1][k], S[wave][F_Y2][k]};
+                const f64 y = (f64)(y0 + r);
+                int xs, xe;
+                row_span(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);
+                if (COUNT) myFrags += (unsigned long long)(xe - xs);
+                if (xs >= xe) continue;
+                const u64 id1 = TT[wave][k];
+                if (ZMODE == 0) {
+#pragma clang loop vectorize(disable) interleave(disable)
+                    for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * TW + lx], id1);
+                    continue;
+                }
+                const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+                const f64 inv = S[wave][F_INV][k];
+                const f64 zz0 = S[wave][F_Z0][k], dz1 = S[wave][F_DZ1][k], dz2 = S[wave][F_DZ2][k];
+                const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
+#pragma clang loop vectorize(disable) interleave(disable)
+                for (int lx = xs; lx < xe; ++lx) {
+                    const f64 dx = (f64)(x0 + lx) - sx[0];
+                    const f64 w1 = (dx * e2y - e2x * dy) * inv;
+                    const f64 w2 = (e1x * dy - dx * e1y) * inv;
+                    const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
+                    const u32 zq = nr_quantize_depth(zz);
+                    const int p = r * TW + lx;
+                    if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
+                    else if (zq < zin[p]) atomicMax(&key[p], id1);
+                }
+            }
+            wave_lds_fence();   // the next chunk overwrites this wave's staging
+        }
+        __syncthreads();
+        for (int p = tid; p < TH * TW; p += VWG) {
+            const int lx = p & (TW - 1), ly = p / TW;
+            if (lx >= wlim || ly >= hlim) continue;
+            u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
+            if (!multi) *g = key[p];
+            else if (ZMODE == 1) atomicMin(g, key[p]);
+            else atomicMax(g, key[p]);
+        }
     }   // work items
     if (COUNT) {
         __syncthreads();
