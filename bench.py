@@ -58,28 +58,26 @@ def make_scene(cfg):
     return xy, z, c
 
 
-def algorithmic_bytes(cfg, n_tri):
+def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True):
     """B = N_tri*S_tri + W*H*(8*ipp + 4*[Z written]),
-    S_tri = 104 B flat / 168 B Gouraud; ipp = 3 (RGB)."""
+    S_tri = 104 B flat / 168 B Gouraud; ipp = 3 (RGB); plus the 3 B/pixel u8
+    frame every step hands over (GetBufferAsUInt8 / GatherFrameU8).  `frac`:
+    the share of the frame one rank owns (tile-row shards)."""
     s_tri = 168 if cfg["gouraud"] else 104
     zw = 4 if cfg.get("write", True) else 0
-    return n_tri * s_tri + cfg["W"] * cfg["H"] * (8 * 3 + zw)
+    return int(frac * (n_tri * s_tri + cfg["W"] * cfg["H"] * (8 * 3 + zw + (3 if u8 else 0))))
 
 
-KERNEL_SYMBOL = {"tile_raster": "k_vis / k_tile_raster", "resolve": "k_resolve"}
+KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)"}
 
 
-def kernel_bytes(cfg, n_tri, path):
-    """Algorithmic bytes each hot kernel must move per launch:
-    order-free path: k_vis reads each triangle's positions and depths once
-    (48 + 24 B); k_resolve writes the framebuffer and depth once
-    (W*H*(8*ipp + 4)).  Ordered path: k_tile_raster does both, plus colours."""
-    W, H = cfg["W"], cfg["H"]
-    zw = 4 if cfg.get("write", True) else 0
-    fb = W * H * (8 * 3 + zw)
-    if path == "order-free":
-        return {"tile_raster": n_tri * (48 + 24), "resolve": fb}
-    return {"tile_raster": algorithmic_bytes(cfg, n_tri)}
+def kernel_bytes(cfg, n_tri, path, frac=1.0):
+    """Algorithmic bytes of the dominant kernel per launch.
+    Both rasterisers read each triangle (positions, depths, colours) once and
+    write the framebuffer and depth once, all inside one kernel (k_vis shades
+    its tiles itself; k_tile_raster keeps the tile in registers); k_vis also
+    writes the u8 frame (k_to_u8_rows does it after the ordered raster)."""
+    return {"tile_raster": algorithmic_bytes(cfg, n_tri, frac, u8=(path == "order-free"))}
 
 
 def cpu_baseline(cfg, xy, z, c, budget_s=10.0, max_frames=50):
@@ -190,7 +188,9 @@ def main():
         if cnt:
             kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
     path = ctx.last_raster_path()
-    kb = kernel_bytes(cfg, n_tri, path)
+    from libnativecpurenderer_amd import sharding
+    frac = len(sharding.owned_rows(H, world, rank)) / H
+    kb = kernel_bytes(cfg, n_tri, path, frac)
     dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
     # (2) timed region: K frames, HIP events only around the dominant kernel
@@ -214,7 +214,7 @@ def main():
     tot, cnt = ctx.get_kernel_timing(dom)
     dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
     achieved = kb[dom] / (dom_us * 1e-6) / 1e9
-    B = algorithmic_bytes(cfg, n_tri)
+    B = algorithmic_bytes(cfg, n_tri)   # whole job
     traffic, pmc = load_pmc_traffic(args.config)
 
     if rank != 0:

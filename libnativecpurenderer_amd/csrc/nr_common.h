@@ -44,9 +44,10 @@ struct TriScratch {
     u64* d_frag = nullptr;                  // device fragment counter
     u32* d_flag = nullptr;                  // device non-opaque flag
     // visibility-buffer raster (nr_tri_free.hip)
-    u32* fcnt = nullptr; u32* foff = nullptr; u32* fsoff = nullptr; u32* fcur = nullptr; size_t ftile_cap = 0;
+    u32* fcnt = nullptr; u32* foff = nullptr; u32* fcur = nullptr; u32* fdone = nullptr; size_t ftile_cap = 0;
+    uint4* fitems = nullptr; size_t fitems_cap = 0;
     u32* flist = nullptr; size_t flist_cap = 0;
-    u64* vis = nullptr; size_t vis_cap = 0;
+    u64* vis = nullptr; size_t vis_cap = 0; int visNeutral = -1;
     u32* dplan = nullptr;
     u32* h_plan = nullptr;                  // pinned, device-mapped copy of the plan totals
     u32* d_hplan = nullptr;                 // its device address

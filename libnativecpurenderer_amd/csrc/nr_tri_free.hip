@@ -17,21 +17,22 @@
 //                    offsets) and of the slice counts (work items)
 //   3 k_free_emit    per-tile lists (order inside a list is irrelevant here)
 //   4 k_vis          one 256-thread workgroup per (tile, slice of <= 512
-//                    triangles): exact row spans -> prefix sum -> fragment-
-//                    parallel depth + LDS atomicMin on the tile's 2048 keys ->
-//                    one coalesced store (or global atomicMin when a long list
-//                    is split over several slices: the load-balancing step for
-//                    mesh poles where thousands of tiny triangles meet)
-//   5 k_resolve      one thread per pixel: winner -> barycentrics -> colour ->
-//                    ApplyPixel -> framebuffer + depth written once; tiles
-//                    with no triangle just receive a pending clear
+//                    triangles; an empty tile is one item): each wave takes
+//                    64-triangle chunks -> exact row spans -> depth + LDS
+//                    atomic on the tile's 2048 packed keys; then the same
+//                    workgroup shades the tile (deferred: winner ->
+//                    barycentrics -> colour -> ApplyPixel -> framebuffer,
+//                    depth and u8 frame written once).  A tile whose list is
+//                    split over several slices (the load-balancing step for
+//                    dense tiles, e.g. mesh poles) merges its keys into `vis`
+//                    with global atomics and the last slice to finish shades
+//                    it and resets those keys.
 #include "nr_tri.h"
 
 namespace nrtri {
 namespace {
 
 constexpr int VWG = 256;     // k_vis workgroup
-constexpr int FCH = 128;     // triangles staged per chunk in k_vis
 constexpr u32 SLICE = 512;   // triangles per work item
 constexpr int TPT = 4;       // triangles per thread in the binning kernels
 constexpr int LDS_HIST_MAX = 16384;
@@ -70,18 +71,24 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
     }
 }
 
-// Single workgroup: off[i] = sum(cnt[<i]), soff[i] = sum(ceil(cnt[<i]/SLICE)),
-// off[ntiles] = P, soff[ntiles] = number of work items; totals = {P, items,
-// number of tiles split over more than one slice}.
-// totals[3] = 1 when the pair list fits `cap`; every later kernel of the
+// Single workgroup: off[i] = sum(cnt[<i]) (off[ntiles] = P) and the work
+// items of k_vis, {tile, list begin, list end, slices of the tile}: an owned
+// tile has max(1, ceil(cnt/SLICE)) of them (an empty tile is one item: k_vis
+// writes its pending clear); totals = {P, items, number of split tiles}.
+// totals[3] = 1 when the pair list fits `cap` and the items `icap`; every later kernel of the
 // batch reads it and does nothing otherwise (the host then re-runs the batch
 // with an exact allocation before anything else is enqueued, nr_settle).
 // It also re-zeroes the tile counters for the next batch (after reading them)
 // and the emit cursors, and mirrors the totals into pinned host memory, so a
 // batch needs no memset and no copy command.
-__global__ __launch_bounds__(1024) void k_free_plan(u32* __restrict__ cnt, int ntiles, u32* __restrict__ off,
-                                                    u32* __restrict__ soff, u32* __restrict__ cur,
-                                                    u32* __restrict__ totals, u32* __restrict__ host_totals, u32 cap) {
+__device__ __forceinline__ u32 tile_items(u32 c, bool owned) {
+    return owned ? (c > SLICE ? (c + SLICE - 1) / SLICE : 1u) : 0u;
+}
+
+__global__ __launch_bounds__(1024) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int nshards,
+                                                    int shard, u32* __restrict__ off, uint4* __restrict__ items,
+                                                    u32* __restrict__ cur, u32* __restrict__ totals,
+                                                    u32* __restrict__ host_totals, u32 cap, u32 icap) {
     __shared__ u32 sA[1024], sB[1024], sC[1024];
     const int tid = threadIdx.x;
     const int per = (ntiles + 1023) / 1024;
@@ -90,7 +97,7 @@ __global__ __launch_bounds__(1024) void k_free_plan(u32* __restrict__ cnt, int n
     for (int i = b0; i < b1; ++i) {
         const u32 c = cnt[i];
         a += c;
-        b += (c + SLICE - 1) / SLICE;
+        b += tile_items(c, owned_row(i / tiles_x, nshards, shard));
         m += c > SLICE ? 1u : 0u;
     }
     sA[tid] = a; sB[tid] = b; sC[tid] = m;
@@ -103,20 +110,25 @@ __global__ __launch_bounds__(1024) void k_free_plan(u32* __restrict__ cnt, int n
         sA[tid] += va; sB[tid] += vb; sC[tid] += vc;
         __syncthreads();
     }
+    const bool fits = sA[1023] <= cap && sB[1023] <= icap;
     u32 ea = sA[tid] - a, eb = sB[tid] - b;
     for (int i = b0; i < b1; ++i) {
         const u32 c = cnt[i];
         off[i] = ea;
-        soff[i] = eb;
+        const u32 ni = tile_items(c, owned_row(i / tiles_x, nshards, shard));
+        if (fits)
+            for (u32 k = 0; k < ni; ++k) {
+                const u32 ls = ea + k * SLICE;
+                items[eb + k] = make_uint4((u32)i, ls, min(ls + SLICE, ea + c), ni);
+            }
         ea += c;
-        eb += (c + SLICE - 1) / SLICE;
+        eb += ni;
         cnt[i] = 0;
         cur[i] = 0;
     }
     if (tid == 1023) {
         off[ntiles] = sA[1023];
-        soff[ntiles] = sB[1023];
-        const u32 t[4] = {sA[1023], sB[1023], sC[1023], sA[1023] <= cap ? 1u : 0u};
+        const u32 t[4] = {sA[1023], sB[1023], sC[1023], fits ? 1u : 0u};
         for (int k = 0; k < 4; ++k) {
             totals[k] = t[k];
             __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -172,20 +184,72 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
     }
 }
 
-// Neutral keys for tiles whose list is split over several slices (their
-// slices merge with global atomics).
-template <int ZMODE>
-__global__ __launch_bounds__(256) void k_vis_init_multi(const FrameParams fp, const u32* __restrict__ off,
-                                                        u64* __restrict__ vis, const u32* __restrict__ plan) {
-    if (!plan[3]) return;
-    const int tile = blockIdx.x;
-    if (off[tile + 1] - off[tile] <= SLICE) return;
-    const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
-    const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
-    for (int p = threadIdx.x; p < TW * TH; p += 256) {
-        const i64 px = x0 + (p & (TW - 1)), py = y0 + p / TW;
-        if (px < fp.W && py < fp.H) vis[py * fp.W + px] = ZMODE == 1 ? ~0ull : 0ull;
+// Deferred shading of one pixel from its packed visibility key (id1 = 0: no
+// fragment won; the pending clears still land).  Winner: barycentrics ->
+// colour -> ApplyPixel -> framebuffer (+ u8 frame) and depth written once.
+template <int ZMODE, bool GOURAUD>
+__device__ __forceinline__ void resolve_pixel(const FrameParams& fp, i64 px, i64 py, u64 kv) {
+    const i64 p = py * fp.W + px;
+    const int ipp = fp.ipp;
+    f64* dst = fp.fb + p * ipp;
+    iu8* d8 = fp.frameU8 ? fp.frameU8 + p * ipp : nullptr;
+    const u32 id1 = (u32)kv;
+    if (id1 == 0) {
+        if (fp.pendColor) {
+            const f64 v = fp.pendColorValue;
+            dst[0] = v; dst[1] = v; dst[2] = v;
+            if (ipp == 4) dst[3] = v;
+            if (d8) {
+                const iu8 v8 = nr_to_u8(v);
+                d8[0] = v8; d8[1] = v8; d8[2] = v8;
+                if (ipp == 4) d8[3] = v8;
+            }
+        }
+        if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+        return;
     }
+    f64 R, G, B, A = 0;
+    if (fp.pendColor) {
+        R = G = B = A = fp.pendColorValue;
+    } else {
+        R = dst[0]; G = dst[1]; B = dst[2];
+        if (ipp == 4) A = dst[3];
+    }
+    (void)A;
+    const i64 t = (i64)id1 - 1;
+    f64 cr, cg, cb, ca;
+    if (GOURAUD) {
+        f64 sx[3], sy[3];
+        tri_screen(fp.src, fp.m, t, sx, sy);
+        const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+        const f64 inv = 1.0 / (e1x * e2y - e2x * e1y);
+        const f64 dx = (f64)px - sx[0], dy = (f64)py - sy[0];
+        const f64 w1 = (dx * e2y - e2x * dy) * inv;
+        const f64 w2 = (e1x * dy - dx * e1y) * inv;
+        const f64* c = fp.src.rgba + t * 12;
+        cr = c[0] + (c[4] - c[0]) * w1 + (c[8] - c[0]) * w2;
+        cg = c[1] + (c[5] - c[1]) * w1 + (c[9] - c[1]) * w2;
+        cb = c[2] + (c[6] - c[2]) * w1 + (c[10] - c[2]) * w2;
+        ca = c[3] + (c[7] - c[3]) * w1 + (c[11] - c[3]) * w2;
+    } else {
+        const f64* c = fp.src.rgba + t * 4;
+        cr = c[0]; cg = c[1]; cb = c[2]; ca = c[3];
+    }
+    // ApplyPixel (cpp:529-547); ca * ct3 == 1 for every batch routed here
+    cr *= fp.ct[0]; cg *= fp.ct[1]; cb *= fp.ct[2]; ca *= fp.ct[3];
+    if (ca != 1) {
+        cr = R * (1 - ca) + cr * ca;
+        cg = G * (1 - ca) + cg * ca;
+        cb = B * (1 - ca) + cb * ca;
+    }
+    dst[0] = cr; dst[1] = cg; dst[2] = cb;
+    if (ipp == 4) dst[3] = ca;
+    if (d8) {
+        d8[0] = nr_to_u8(cr); d8[1] = nr_to_u8(cg); d8[2] = nr_to_u8(cb);
+        if (ipp == 4) d8[3] = nr_to_u8(ca);
+    }
+    if (ZMODE == 1) fp.depth[p] = (u32)(kv >> 32);
+    else if (ZMODE == 2 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
 }
 
 enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
@@ -205,10 +269,11 @@ __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOM
 //           lane writes its triangle's lane index into a row->triangle map
 //   rows    the chunk's (triangle, row) items over the 64 lanes: exact span
 //           (row_span), then per pixel depth + LDS atomic on the packed key
-template <int ZMODE, bool COUNT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
-__global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __restrict__ off,
-                                             const u32* __restrict__ soff, const u32* __restrict__ list,
-                                             u64* __restrict__ vis, const u32* __restrict__ plan) {
+template <int ZMODE, bool COUNT, bool GOURAUD>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+__global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
+                                             const u32* __restrict__ list,
+                                             u64* __restrict__ vis, u32* __restrict__ done,
+                                             const u32* __restrict__ plan) {
     constexpr bool DEPTH = ZMODE != 0;
     __shared__ u64 key[TH * TW];
     __shared__ u32 zin[ZMODE == 2 ? TH * TW : 1];
@@ -217,37 +282,34 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     __shared__ iu8 RR0[NW][64];
     __shared__ unsigned short ROFF[NW][64];
     __shared__ u32 TT[NW][64];   // triangle id + 1 of each lane's triangle
-    __shared__ int sTile;
+    __shared__ int sLast;
     __shared__ unsigned long long sFrag;
     if (!plan[3]) return;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int ntiles = fp.tiles_x * fp.tiles_y;
     const u32 nitems = plan[1];
     unsigned long long myFrags = 0;
     if (COUNT && tid == 0) sFrag = 0;
     // grid-stride over the work items (the grid is sized from a capacity
     // bound, not from the item count, so no host sync is needed)
+    uint4 dnext = blockIdx.x < nitems ? items[blockIdx.x] : make_uint4(0, 0, 0, 0);
     for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const uint4 d = dnext;
+        if (item + gridDim.x < nitems) dnext = items[item + gridDim.x];
         __syncthreads();
-        if (tid == 0) {   // tile of this work item: last tile with soff[tile] <= item
-            int lo = 0, hi = ntiles;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (soff[mid] <= item) lo = mid; else hi = mid;
-            }
-            sTile = lo;
-        }
-        __syncthreads();
-        const int tile = sTile;
-        const u32 t0 = off[tile], t1 = off[tile + 1];
-        const u32 slice = item - soff[tile];
-        const u32 ls = t0 + slice * SLICE;
-        const u32 le = ls + SLICE < t1 ? ls + SLICE : t1;
-        const bool multi = t1 - t0 > SLICE;
+        const int tile = (int)d.x;
+        const u32 ls = d.y, le = d.z;
+        const bool multi = d.w > 1;
         const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
         const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
+        if (ls == le) {   // no triangle: only the pending clears
+            for (int p = tid; p < TH * TW; p += VWG) {
+                const int lx = p & (TW - 1), ly = p / TW;
+                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, 0ull);
+            }
+            continue;
+        }
 
         for (int p = tid; p < TH * TW; p += VWG) {
             const int lx = p & (TW - 1), ly = p / TW;
@@ -358,13 +420,43 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
             wave_lds_fence();   // the next chunk overwrites this wave's staging
         }
         __syncthreads();
+        if (!multi) {   // the whole list was in this slice: shade now
+            for (int p = tid; p < TH * TW; p += VWG) {
+                const int lx = p & (TW - 1), ly = p / TW;
+                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[p]);
+            }
+            continue;
+        }
+        // split tile: merge into the global keys; the last slice to finish
+        // shades the tile and puts its keys back to the neutral value.
+        // Hand-off without cache-wide fences (an agent-scope release writes
+        // back the whole L2): the keys only ever move through device-scope
+        // atomics and sc1 loads/stores, each wave drains its atomics before
+        // the barrier, and the slice counter is a relaxed device atomic.
         for (int p = tid; p < TH * TW; p += VWG) {
             const int lx = p & (TW - 1), ly = p / TW;
             if (lx >= wlim || ly >= hlim) continue;
             u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-            if (!multi) *g = key[p];
-            else if (ZMODE == 1) atomicMin(g, key[p]);
+            if (ZMODE == 1) atomicMin(g, key[p]);
             else atomicMax(g, key[p]);
+        }
+        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: this wave's atomics performed
+        __syncthreads();
+        if (tid == 0) {
+            const u32 nsl = d.w;
+            const u32 prev = __hip_atomic_fetch_add(&done[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sLast = prev + 1 == nsl;
+            if (prev + 1 == nsl) __hip_atomic_store(&done[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!sLast) continue;
+        for (int p = tid; p < TH * TW; p += VWG) {
+            const int lx = p & (TW - 1), ly = p / TW;
+            if (lx >= wlim || ly >= hlim) continue;
+            u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
+            const u64 kv = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, kv);
+            __hip_atomic_store(g, ZMODE == 1 ? ~0ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }   // work items
     if (COUNT) {
@@ -375,105 +467,16 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const u32* __
     }
 }
 
-// One thread per pixel (2-D grid: x blocks of 256, one row per blockIdx.y).
-template <int ZMODE, bool GOURAUD>
-__global__ __launch_bounds__(256) void k_resolve(const FrameParams fp, const u32* __restrict__ off,
-                                                 const u64* __restrict__ vis, const u32* __restrict__ plan) {
-    if (!plan[3]) return;
-    const i64 px = (i64)blockIdx.x * 256 + threadIdx.x;
-    // blockIdx.y enumerates the rows of the owned tile rows only
-    const i64 py = ((i64)(blockIdx.y / TH) * fp.nshards + fp.shard) * TH + blockIdx.y % TH;
-    if (px >= fp.W || py >= fp.H) return;
-    const int tile = (int)(py / TH) * fp.tiles_x + (int)(px / TW);
-    const i64 p = py * fp.W + px;
-    const int ipp = fp.ipp;
-    f64* dst = fp.fb + p * ipp;
-    iu8* d8 = fp.frameU8 ? fp.frameU8 + p * ipp : nullptr;
-    if (off[tile + 1] == off[tile]) {   // no triangle touches this tile
-        if (fp.pendColor) {
-            const f64 v = fp.pendColorValue;
-            dst[0] = v; dst[1] = v; dst[2] = v;
-            if (ipp == 4) dst[3] = v;
-            if (d8) {
-                const iu8 v8 = nr_to_u8(v);
-                d8[0] = v8; d8[1] = v8; d8[2] = v8;
-                if (ipp == 4) d8[3] = v8;
-            }
-        }
-        if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
-        return;
-    }
-    const u64 kv = vis[p];
-    const u32 id1 = (u32)kv;
-    if (id1 == 0) {
-        if (fp.pendColor) {
-            const f64 v = fp.pendColorValue;
-            dst[0] = v; dst[1] = v; dst[2] = v;
-            if (ipp == 4) dst[3] = v;
-            if (d8) {
-                const iu8 v8 = nr_to_u8(v);
-                d8[0] = v8; d8[1] = v8; d8[2] = v8;
-                if (ipp == 4) d8[3] = v8;
-            }
-        }
-        if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
-        return;
-    }
-    f64 R, G, B, A = 0;
-    if (fp.pendColor) {
-        R = G = B = A = fp.pendColorValue;
-    } else {
-        R = dst[0]; G = dst[1]; B = dst[2];
-        if (ipp == 4) A = dst[3];
-    }
-    const i64 t = (i64)id1 - 1;
-    f64 cr, cg, cb, ca;
-    if (GOURAUD) {
-        f64 sx[3], sy[3];
-        tri_screen(fp.src, fp.m, t, sx, sy);
-        const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-        const f64 inv = 1.0 / (e1x * e2y - e2x * e1y);
-        const f64 dx = (f64)px - sx[0], dy = (f64)py - sy[0];
-        const f64 w1 = (dx * e2y - e2x * dy) * inv;
-        const f64 w2 = (e1x * dy - dx * e1y) * inv;
-        const f64* c = fp.src.rgba + t * 12;
-        cr = c[0] + (c[4] - c[0]) * w1 + (c[8] - c[0]) * w2;
-        cg = c[1] + (c[5] - c[1]) * w1 + (c[9] - c[1]) * w2;
-        cb = c[2] + (c[6] - c[2]) * w1 + (c[10] - c[2]) * w2;
-        ca = c[3] + (c[7] - c[3]) * w1 + (c[11] - c[3]) * w2;
-    } else {
-        const f64* c = fp.src.rgba + t * 4;
-        cr = c[0]; cg = c[1]; cb = c[2]; ca = c[3];
-    }
-    // ApplyPixel (cpp:529-547); ca * ct3 == 1 for every batch routed here
-    cr *= fp.ct[0]; cg *= fp.ct[1]; cb *= fp.ct[2]; ca *= fp.ct[3];
-    if (ca != 1) {
-        cr = R * (1 - ca) + cr * ca;
-        cg = G * (1 - ca) + cg * ca;
-        cb = B * (1 - ca) + cb * ca;
-    }
-    dst[0] = cr; dst[1] = cg; dst[2] = cb;
-    if (ipp == 4) dst[3] = ca;
-    if (d8) {
-        d8[0] = nr_to_u8(cr); d8[1] = nr_to_u8(cg); d8[2] = nr_to_u8(cb);
-        if (ipp == 4) d8[3] = nr_to_u8(ca);
-    }
-    if (ZMODE == 1) fp.depth[p] = (u32)(kv >> 32);
-    else if (ZMODE == 2 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
-}
-
-template <int Z, bool C>
-void launch_vis(const FrameParams& fp, const u32* off, const u32* soff, const u32* list, u64* vis, u32 grid,
-                const u32* plan, hipStream_t s) {
-    hipLaunchKernelGGL((k_vis<Z, C>), dim3(grid), dim3(VWG), 0, s, fp, off, soff, list, vis, plan);
+template <int Z, bool C, bool G>
+void launch_vis(const FrameParams& fp, const TriScratch& sc, u32 grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_vis<Z, C, G>), dim3(grid), dim3(VWG), 0, s, fp, sc.fitems, sc.flist, sc.vis, sc.fdone,
+                       sc.dplan);
 }
 
 template <int Z, bool G>
-void launch_resolve(const FrameParams& fp, const u32* off, const u64* vis, const u32* plan, hipStream_t s) {
-    const int owned = (fp.tiles_y - fp.shard + fp.nshards - 1) / fp.nshards;
-    if (owned <= 0) return;
-    dim3 grid((unsigned)((fp.W + 255) / 256), (unsigned)(owned * TH));
-    hipLaunchKernelGGL((k_resolve<Z, G>), grid, dim3(256), 0, s, fp, off, vis, plan);
+void launch_vis_z(const FrameParams& fp, const TriScratch& sc, u32 grid, hipStream_t s) {
+    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, grid, s);
+    else launch_vis<Z, false, G>(fp, sc, grid, s);
 }
 
 // Everything a batch needs to be re-run after an overflow (nr_settle).
@@ -494,13 +497,14 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
     const bool g = src.gouraud != 0;
 
-    u32* tb[4] = {sc.fcnt, sc.foff, sc.fsoff, sc.fcur};
+    u32* tb[4] = {sc.fcnt, sc.foff, sc.fcur, sc.fdone};
     const size_t oldcap = sc.ftile_cap;
     if (!grow_set(tb, &sc.ftile_cap, (size_t)ntiles + 1)) return false;
-    sc.fcnt = tb[0]; sc.foff = tb[1]; sc.fsoff = tb[2]; sc.fcur = tb[3];
+    sc.fcnt = tb[0]; sc.foff = tb[1]; sc.fcur = tb[2]; sc.fdone = tb[3];
     if (sc.ftile_cap != oldcap) {   // counters start at zero; k_free_plan re-zeroes them after each use
         NR_CHECK(hipMemsetAsync(sc.fcnt, 0, sc.ftile_cap * sizeof(u32), s));
         NR_CHECK(hipMemsetAsync(sc.fcur, 0, sc.ftile_cap * sizeof(u32), s));
+        NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.ftile_cap * sizeof(u32), s));
     }
     if (!sc.dplan) NR_CHECK(hipMalloc(&sc.dplan, 4 * sizeof(u32)));
     if (!sc.h_plan) {
@@ -508,52 +512,78 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         NR_CHECK(hipHostGetDevicePointer((void**)&sc.d_hplan, sc.h_plan, 0));
     }
     u64* vb[1] = {sc.vis};
+    const size_t oldvis = sc.vis_cap;
     if (!grow_set(vb, &sc.vis_cap, (size_t)(ctx->width * ctx->height))) return false;
     sc.vis = vb[0];
+    // keys of split tiles merge into `vis`, which every batch leaves at the
+    // neutral value of its depth mode; refill only when the mode changes
+    const int neutral = zmode == 1 ? 1 : 0;
+    if (sc.vis_cap != oldvis || sc.visNeutral != neutral) {
+        NR_CHECK(hipMemsetD32Async((hipDeviceptr_t)sc.vis, neutral ? 0xFFFFFFFFu : 0u, sc.vis_cap * 2, s));
+        sc.visNeutral = neutral;
+    }
 
-    size_t cap = 0xFFFFFFFFull;
+    auto grow_list = [&](size_t need) {
+        u32* lb[1] = {sc.flist};
+        const bool ok = grow_set(lb, &sc.flist_cap, std::max<size_t>(need, 1));
+        sc.flist = lb[0];
+        return ok;
+    };
+    auto grow_items = [&](size_t need) {
+        uint4* ib[1] = {sc.fitems};
+        const bool ok = grow_set(ib, &sc.fitems_cap, std::max<size_t>(need, 1));
+        sc.fitems = ib[0];
+        return ok;
+    };
+    size_t cap;
     if (!exact) {
         const u64 est = std::max<u64>(std::max<u64>(sc.lastPairs + sc.lastPairs / 4, (u64)src.n * 2), 1u << 20);
         cap = (size_t)std::min<u64>(sc.capOverride ? sc.capOverride : est, 0xFFFFFFF0ull);
-        u32* lb[1] = {sc.flist};
-        if (!grow_set(lb, &sc.flist_cap, cap)) return false;
-        sc.flist = lb[0];
+        if (!grow_list(cap)) return false;
         if (!sc.capOverride) cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
+        // work items: at most one per tile + one per full slice of the list
+        if (!grow_items((size_t)ntiles + cap / SLICE + 2)) return false;
+    } else {
+        if (!grow_list(1) || !grow_items(1)) return false;
+        cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
     }
 
     const bool ldsh = ntiles <= LDS_HIST_MAX;
     const size_t hbytes = ldsh ? (size_t)ntiles * sizeof(u32) : 0;
     const int gb = (int)((src.n + 256 * TPT - 1) / (256 * TPT));
     hipEvent_t e0, e1;
-    nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
-    if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.fcnt, ntiles);
-    else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, s, bp, sc.fcnt, ntiles);
-    NR_CHECK(hipGetLastError());
-    nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
-
-    nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
-    hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, sc.foff, sc.fsoff, sc.fcur, sc.dplan,
-                       sc.d_hplan, (u32)cap);
-    NR_CHECK(hipGetLastError());
-    nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
-
     u32 grid;
-    bool multi = true;
-    if (exact) {
+    for (int attempt = 0;; ++attempt) {
+        nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
+        if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.fcnt, ntiles);
+        else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, s, bp, sc.fcnt, ntiles);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
+
+        nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
+        hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, fp.tiles_x, fp.nshards,
+                           fp.shard, sc.foff, sc.fitems, sc.fcur, sc.dplan, sc.d_hplan, (u32)cap,
+                           (u32)std::min<size_t>(sc.fitems_cap, 0xFFFFFFF0ull));
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
+
+        if (!exact) {
+            if (!sc.planEvent) NR_CHECK(hipEventCreateWithFlags(&sc.planEvent, hipEventDisableTiming));
+            NR_CHECK(hipEventRecord(sc.planEvent, s));
+            grid = (u32)std::min<u64>(sc.fitems_cap, 8192);   // grid-stride over the items
+            break;
+        }
+        // exact: read the totals back; if the list or the items did not fit,
+        // grow both and bin again (the plan kernel re-zeroed the counters)
         NR_CHECK(hipStreamSynchronize(s));
-        const u32 P = sc.h_plan[0];
+        sc.lastPairs = sc.h_plan[0];
         grid = sc.h_plan[1];
-        multi = sc.h_plan[2] != 0;
-        sc.lastPairs = P;
-        u32* lb[1] = {sc.flist};
-        if (!grow_set(lb, &sc.flist_cap, (size_t)std::max<u32>(P, 1))) return false;
-        sc.flist = lb[0];
-    } else {
-        if (!sc.planEvent) NR_CHECK(hipEventCreateWithFlags(&sc.planEvent, hipEventDisableTiming));
-        NR_CHECK(hipEventRecord(sc.planEvent, s));
-        // a bound on the work items: every non-empty tile + one per full slice
-        const u64 bound = (u64)ntiles + cap / SLICE + 1;
-        grid = (u32)std::min<u64>(bound, 8192);
+        if (sc.h_plan[3]) break;
+        if (attempt > 0 || !grow_list(sc.h_plan[0]) || !grow_items(sc.h_plan[1])) {
+            nr_set_error_msg("triangle binning: pair list allocation failed");
+            return false;
+        }
+        cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
     }
 
     nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
@@ -562,30 +592,14 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
 
-    if (multi) {
-        nr_timing_begin(ctx, NRK_VIS_INIT, &e0, &e1);
-        if (zmode == 1) hipLaunchKernelGGL(k_vis_init_multi<1>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis, sc.dplan);
-        else hipLaunchKernelGGL(k_vis_init_multi<0>, dim3(ntiles), dim3(256), 0, s, fp, sc.foff, sc.vis, sc.dplan);
-        NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_VIS_INIT, e0, e1);
-    }
-
     if (grid > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-        const bool C = fp.fragCounter != nullptr;
-        if (zmode == 1) { if (C) launch_vis<1, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); else launch_vis<1, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); }
-        else if (zmode == 2) { if (C) launch_vis<2, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); else launch_vis<2, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); }
-        else { if (C) launch_vis<0, true>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); else launch_vis<0, false>(fp, sc.foff, sc.fsoff, sc.flist, sc.vis, grid, sc.dplan, s); }
+        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, grid, s); else launch_vis_z<1, false>(fp, sc, grid, s); }
+        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, grid, s); else launch_vis_z<2, false>(fp, sc, grid, s); }
+        else { if (g) launch_vis_z<0, true>(fp, sc, grid, s); else launch_vis_z<0, false>(fp, sc, grid, s); }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
     }
-
-    nr_timing_begin(ctx, NRK_RESOLVE, &e0, &e1);
-    if (zmode == 1) { if (g) launch_resolve<1, true>(fp, sc.foff, sc.vis, sc.dplan, s); else launch_resolve<1, false>(fp, sc.foff, sc.vis, sc.dplan, s); }
-    else if (zmode == 2) { if (g) launch_resolve<2, true>(fp, sc.foff, sc.vis, sc.dplan, s); else launch_resolve<2, false>(fp, sc.foff, sc.vis, sc.dplan, s); }
-    else { if (g) launch_resolve<0, true>(fp, sc.foff, sc.vis, sc.dplan, s); else launch_resolve<0, false>(fp, sc.foff, sc.vis, sc.dplan, s); }
-    NR_CHECK(hipGetLastError());
-    nr_timing_end(ctx, NRK_RESOLVE, e0, e1);
     return true;
 }
 
