@@ -201,6 +201,14 @@ __host__ __device__ __forceinline__ u32 nr_quantize_depth(f64 z) {
     return (u32)(z * 4294967295.0);
 }
 
+// The same function without branches: clamping the product to
+// [0, 4294967295] maps z <= 0 (and NaN: fmax drops it) to 0 and z >= 1 (and
+// +inf) to 0xFFFFFFFF, and leaves every in-range product (hence its
+// truncation) unchanged.
+__device__ __forceinline__ u32 nr_quantize_depth_bl(f64 z) {
+    return (u32)fmin(fmax(z * 4294967295.0, 0.0), 4294967295.0);
+}
+
 // cpp:52-57: (iu8)(v*255) = cvttsd2si to int32, keep the low byte (A.5)
 __device__ __forceinline__ iu8 nr_to_u8(f64 v) {
     f64 t = v * 255;

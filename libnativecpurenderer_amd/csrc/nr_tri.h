@@ -109,6 +109,31 @@ __device__ __forceinline__ void row_span(const f64 (&sx)[3], const f64 (&sy)[3],
     }
 }
 
+// row_span for a row known to lie in [ceil(ymin), ceil(ymax)) (ymin <= y <
+// ymax), without branches.  There exactly one vertex v is on its own side of
+// y (sy[v] > y differs from the other two), and the two straddling edges are
+// the two edges at v; in pointInPolygon's (i, j) orientation those are
+// v=0: (0,2) (1,0)   v=1: (2,1) (1,0)   v=2: (0,2) (2,1).
+// The crossings are evaluated with the same expression, and min/max does not
+// depend on which edge comes first, so the span equals row_span's.
+__device__ __forceinline__ void row_span_in(const f64 (&sx)[3], const f64 (&sy)[3], f64 y, f64 x0, f64 wlim,
+                                            int& xs, int& xe) {
+    const bool b0 = sy[0] > y, b1 = sy[1] > y, b2 = sy[2] > y;
+    const bool v1 = (b1 != b0) && (b1 != b2);
+    const bool v2 = (b2 != b0) && (b2 != b1);
+    // edge A: v==1 ? (2,1) : (0,2);  edge B: v==2 ? (2,1) : (1,0)
+    const f64 aix = v1 ? sx[2] : sx[0], aiy = v1 ? sy[2] : sy[0];
+    const f64 ajx = v1 ? sx[1] : sx[2], ajy = v1 ? sy[1] : sy[2];
+    const f64 bix = v2 ? sx[2] : sx[1], biy = v2 ? sy[2] : sy[1];
+    const f64 bjx = v2 ? sx[1] : sx[0], bjy = v2 ? sy[1] : sy[0];
+    const f64 ca = (ajx - aix) * (y - aiy) / (ajy - aiy) + aix;
+    const f64 cb = (bjx - bix) * (y - biy) / (bjy - biy) + bix;
+    const f64 lo = fmin(ca, cb), hi = fmax(ca, cb);
+    xs = (int)clampd(ceil(lo) - x0, 0.0, wlim);
+    xe = (int)clampd(ceil(hi) - x0, 0.0, wlim);
+    if (xe < xs) xe = xs;
+}
+
 // State snapshot of one draw call (passed by value to the kernels).
 struct FrameParams {
     TriSrc src;

@@ -33,7 +33,10 @@ namespace nrtri {
 namespace {
 
 constexpr int VWG = 256;     // k_vis workgroup
-constexpr u32 SLICE = 512;   // triangles per work item
+#ifndef NR_SLICE
+#define NR_SLICE 1024
+#endif
+constexpr u32 SLICE = NR_SLICE;   // triangles per work item
 constexpr int TPT = 4;       // triangles per thread in the binning kernels
 constexpr int LDS_HIST_MAX = 16384;
 
@@ -390,9 +393,9 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const uint4* 
                 const int r = RR0[wave][k] + (it - ROFF[wave][k]);
                 const f64 sx[3] = {S[wave][F_X0][k], S[wave][F_X1][k], S[wave][F_X2][k]};
                 const f64 sy[3] = {S[wave][F_Y0][k], S[wave][F_Y1][k], S[wave][F_Y2][k]};
-                const f64 y = (f64)(y0 + r);
+                const f64 y = (f64)(int)(y0 + r);
                 int xs, xe;
-                row_span(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);
+                row_span_in(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);
                 if (COUNT) myFrags += (unsigned long long)(xe - xs);
                 if (xs >= xe) continue;
                 const u64 id1 = TT[wave][k];
@@ -405,13 +408,14 @@ __global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const uint4* 
                 const f64 inv = S[wave][F_INV][k];
                 const f64 zz0 = S[wave][F_Z0][k], dz1 = S[wave][F_DZ1][k], dz2 = S[wave][F_DZ2][k];
                 const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
+                f64 X = (f64)(int)(x0 + xs);   // pixel x as f64, exact (integers < 2^31)
 #pragma clang loop vectorize(disable) interleave(disable)
-                for (int lx = xs; lx < xe; ++lx) {
-                    const f64 dx = (f64)(x0 + lx) - sx[0];
+                for (int lx = xs; lx < xe; ++lx, X += 1.0) {
+                    const f64 dx = X - sx[0];
                     const f64 w1 = (dx * e2y - e2x * dy) * inv;
                     const f64 w2 = (e1x * dy - dx * e1y) * inv;
                     const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
-                    const u32 zq = nr_quantize_depth(zz);
+                    const u32 zq = nr_quantize_depth_bl(zz);
                     const int p = r * TW + lx;
                     if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
                     else if (zq < zin[p]) atomicMax(&key[p], id1);

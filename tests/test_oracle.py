@@ -179,6 +179,18 @@ def py_row_span(y, pts):
     return math.ceil(min(c)), math.ceil(max(c))
 
 
+def py_row_span_in(y, pts):
+    """nr_tri.h row_span_in: for ymin <= y < ymax, the two edges at the vertex
+    alone on its side of y, in pointInPolygon's (i, j) orientation."""
+    b = [p[1] > y for p in pts]
+    v1 = b[1] != b[0] and b[1] != b[2]
+    v2 = b[2] != b[0] and b[2] != b[1]
+    a = (2, 1) if v1 else (0, 2)
+    bb = (2, 1) if v2 else (1, 0)
+    c = [(pts[j][0] - pts[i][0]) * (y - pts[i][1]) / (pts[j][1] - pts[i][1]) + pts[i][0] for i, j in (a, bb)]
+    return math.ceil(min(c)), math.ceil(max(c))
+
+
 def _edge_case_triangles():
     g = scenes.rng(77)
     tris = [
@@ -200,6 +212,13 @@ def test_row_span_rule_equals_point_in_polygon():
             lo, hi = py_row_span(float(y), pts)
             for x in range(-4, 18):
                 assert py_point_in_polygon(float(x), float(y), pts) == (lo <= x < hi), (pts, x, y)
+
+
+def test_branchless_row_span_equals_row_span():
+    for pts in _edge_case_triangles():
+        ys = [p[1] for p in pts]
+        for y in range(math.ceil(min(ys)), math.ceil(max(ys))):
+            assert py_row_span_in(float(y), pts) == py_row_span(float(y), pts), (pts, y)
 
 
 def test_oracle_triangle_coverage_equals_point_in_polygon(oracle):
