@@ -32,7 +32,13 @@
 namespace nrtri {
 namespace {
 
-constexpr int VWG = 256;     // k_vis workgroup
+#ifndef NR_VWG
+#define NR_VWG 256
+#endif
+#ifndef NR_VIS_WAVES_PER_EU
+#define NR_VIS_WAVES_PER_EU 1
+#endif
+constexpr int VWG = NR_VWG;  // k_vis workgroup
 #ifndef NR_SLICE
 #define NR_SLICE 1024
 #endif
@@ -273,7 +279,7 @@ __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOM
 //   rows    the chunk's (triangle, row) items over the 64 lanes: exact span
 //           (row_span), then per pixel depth + LDS atomic on the packed key
 template <int ZMODE, bool COUNT, bool GOURAUD>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
-__global__ __launch_bounds__(VWG) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
+__global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES_PER_EU))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ vis, u32* __restrict__ done,
                                              const u32* __restrict__ plan) {
