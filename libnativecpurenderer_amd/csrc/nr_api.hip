@@ -321,7 +321,7 @@ void DestroyRenderContext(RenderContext* ctx) {
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
                     t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
-                    t.fcnt,      t.foff,       t.fitems,   t.fcur, t.fdone, t.flist, t.vis,  t.dplan, ctx->frameU8};
+                    t.fcnt,      t.foff,       t.fitems,   t.fcur, t.fdone, t.frect, t.flist, t.vis,  t.dplan, ctx->frameU8};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));

@@ -46,6 +46,7 @@ struct TriScratch {
     // visibility-buffer raster (nr_tri_free.hip)
     u32* fcnt = nullptr; u32* foff = nullptr; u32* fcur = nullptr; u32* fdone = nullptr; size_t ftile_cap = 0;
     uint4* fitems = nullptr; size_t fitems_cap = 0;
+    u64* frect = nullptr; size_t frect_cap = 0;   // per-triangle tile rectangle (count -> emit)
     u32* flist = nullptr; size_t flist_cap = 0;
     u64* vis = nullptr; size_t vis_cap = 0; int visNeutral = -1;
     u32* dplan = nullptr;

@@ -42,9 +42,32 @@ __device__ __forceinline__ bool owned_row(int ty, int nshards, int shard) { retu
 
 __device__ __forceinline__ f64 clampd(f64 v, f64 lo, f64 hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Triangle arrays are 16-byte aligned (hipMalloc'd, or staged by the draw
+// entry points): a triangle's 6 positions / 12 or 4 colours load as 16-byte
+// vectors, 3 or 6 or 2 loads instead of 6 or 12 or 4.
+__device__ __forceinline__ void load_tri_xy(const f64* xy, i64 t, f64 (&v)[6]) {
+    const double2* q = reinterpret_cast<const double2*>(xy + t * 6);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double2 a = q[k];
+        v[2 * k] = a.x; v[2 * k + 1] = a.y;
+    }
+}
+
+template <int N>   // 4 (flat) or 12 (Gouraud)
+__device__ __forceinline__ void load_tri_rgba(const f64* rgba, i64 t, f64 (&c)[N]) {
+    const double2* q = reinterpret_cast<const double2*>(rgba + t * N);
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) {
+        const double2 a = q[k];
+        c[2 * k] = a.x; c[2 * k + 1] = a.y;
+    }
+}
+
 // Screen-space vertices of triangle t (cpp:446-453 applied to each vertex).
 __device__ __forceinline__ void tri_screen(const TriSrc& s, const f64* m, i64 t, f64 (&sx)[3], f64 (&sy)[3]) {
-    const f64* p = s.xy + t * 6;
+    f64 p[6];
+    load_tri_xy(s.xy, t, p);
 #pragma unroll
     for (int v = 0; v < 3; ++v) nr_xform(m, p[2 * v], p[2 * v + 1], sx[v], sy[v]);
 }

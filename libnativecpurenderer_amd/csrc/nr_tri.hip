@@ -161,6 +161,23 @@ void GetDepthBuffer(RenderContext* ctx, u32* out) {
 // New: triangles from device-resident arrays (xy n*6, z n*3 or NULL,
 // rgba n*4 flat / n*12 Gouraud), in the context's transform.
 void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud) {
+    // the kernels load positions and colours as 16-byte vectors: re-stage
+    // arrays that are not 16-byte aligned (device-to-device copy)
+    if ((((uintptr_t)xy | (uintptr_t)rgba) & 15) && n > 0) {
+        NR_CHECK(hipSetDevice(ctx->device));
+        settle(ctx);
+        const size_t ncol = gouraud ? 12 : 4, zn = ((size_t)n * 3 + 1) & ~(size_t)1;
+        f64* stage_buf[1] = {ctx->tri.stage};
+        if (!grow_set(stage_buf, &ctx->tri.stage_cap, (size_t)n * (6 + ncol) + zn)) return;
+        ctx->tri.stage = stage_buf[0];
+        f64* dxy = ctx->tri.stage;
+        f64* dz = dxy + (size_t)n * 6;
+        f64* dc = dz + zn;
+        NR_CHECK(hipMemcpyAsync(dxy, xy, (size_t)n * 6 * sizeof(f64), hipMemcpyDeviceToDevice, ctx->stream));
+        NR_CHECK(hipMemcpyAsync(dc, rgba, (size_t)n * ncol * sizeof(f64), hipMemcpyDeviceToDevice, ctx->stream));
+        draw(ctx, dxy, z, dc, n, gouraud, OPQ_UNKNOWN);
+        return;
+    }
     draw(ctx, xy, z, rgba, n, gouraud, OPQ_UNKNOWN);
 }
 
@@ -170,13 +187,14 @@ void DrawTriangles(RenderContext* ctx, const f64* xy, const f64* z, const f64* r
     settle(ctx);   // a pending batch may still read the staging buffer
     if (n <= 0) return;
     const size_t ncol = gouraud ? 12 : 4;
-    const size_t need = (size_t)n * (6 + 3 + ncol);
+    const size_t zn = ((size_t)n * 3 + 1) & ~(size_t)1;   // keeps the colours 16-byte aligned
+    const size_t need = (size_t)n * (6 + ncol) + zn;
     f64* stage_buf[1] = {ctx->tri.stage};
     if (!grow_set(stage_buf, &ctx->tri.stage_cap, need)) return;
     ctx->tri.stage = stage_buf[0];
     f64* dxy = ctx->tri.stage;
     f64* dz = dxy + (size_t)n * 6;
-    f64* dc = dz + (size_t)n * 3;
+    f64* dc = dz + zn;
     NR_CHECK(hipMemcpyAsync(dxy, xy, (size_t)n * 6 * sizeof(f64), hipMemcpyHostToDevice, ctx->stream));
     if (z) NR_CHECK(hipMemcpyAsync(dz, z, (size_t)n * 3 * sizeof(f64), hipMemcpyHostToDevice, ctx->stream));
     NR_CHECK(hipMemcpyAsync(dc, rgba, (size_t)n * ncol * sizeof(f64), hipMemcpyHostToDevice, ctx->stream));

@@ -46,8 +46,16 @@ constexpr u32 SLICE = NR_SLICE;   // triangles per work item
 constexpr int TPT = 4;       // triangles per thread in the binning kernels
 constexpr int LDS_HIST_MAX = 16384;
 
+// Tile rectangle of a triangle, packed for the emit pass (16 bits per bound;
+// NO_RECT: the triangle produces no fragment).
+constexpr u64 NO_RECT = ~0ull;
+__device__ __forceinline__ u64 pack_rect(int tx0, int tx1, int ty0, int ty1) {
+    return (u64)(u32)tx0 | ((u64)(u32)tx1 << 16) | ((u64)(u32)ty0 << 32) | ((u64)(u32)ty1 << 48);
+}
+
 template <bool LDSH>
-__global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __restrict__ tile_cnt, int ntiles) {
+__global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __restrict__ tile_cnt, int ntiles,
+                                                    u64* __restrict__ rects) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
     if (LDSH) {
@@ -61,7 +69,9 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
         f64 sx[3], sy[3];
         tri_screen(bp.src, bp.m, t, sx, sy);
         int tx0, tx1, ty0, ty1;
-        if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
+        const bool hit = tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1);
+        rects[t] = hit ? pack_rect(tx0, tx1, ty0, ty1) : NO_RECT;
+        if (!hit) continue;
         for (int ty = ty0; ty <= ty1; ++ty) {
             if (!owned_row(ty, bp.nshards, bp.shard)) continue;
             for (int tx = tx0; tx <= tx1; ++tx) {
@@ -148,7 +158,7 @@ __global__ __launch_bounds__(1024) void k_free_plan(u32* __restrict__ cnt, int n
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32* __restrict__ off,
                                                    u32* __restrict__ cur, u32* __restrict__ list, int ntiles,
-                                                   const u32* __restrict__ plan) {
+                                                   const u64* __restrict__ rects, const u32* __restrict__ plan) {
     extern __shared__ u32 hist[];
     if (!plan[3]) return;
     const int tid = threadIdx.x;
@@ -159,10 +169,10 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
         for (int k = 0; k < TPT; ++k) {
             const i64 t = base + k * 256 + tid;
             if (t >= bp.src.n) break;
-            f64 sx[3], sy[3];
-            tri_screen(bp.src, bp.m, t, sx, sy);
-            int tx0, tx1, ty0, ty1;
-            if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
+            const u64 rc = rects[t];
+            if (rc == NO_RECT) continue;
+            const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
+            const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
             for (int ty = ty0; ty <= ty1; ++ty)
                 if (owned_row(ty, bp.nshards, bp.shard))
                     for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * bp.tiles_x + tx], 1u);
@@ -178,10 +188,10 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
         if (t >= bp.src.n) break;
-        f64 sx[3], sy[3];
-        tri_screen(bp.src, bp.m, t, sx, sy);
-        int tx0, tx1, ty0, ty1;
-        if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
+        const u64 rc = rects[t];
+        if (rc == NO_RECT) continue;
+        const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
+        const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
         for (int ty = ty0; ty <= ty1; ++ty) {
             if (!owned_row(ty, bp.nshards, bp.shard)) continue;
             for (int tx = tx0; tx <= tx1; ++tx) {
@@ -235,13 +245,15 @@ __device__ __forceinline__ void resolve_pixel(const FrameParams& fp, i64 px, i64
         const f64 dx = (f64)px - sx[0], dy = (f64)py - sy[0];
         const f64 w1 = (dx * e2y - e2x * dy) * inv;
         const f64 w2 = (e1x * dy - dx * e1y) * inv;
-        const f64* c = fp.src.rgba + t * 12;
+        f64 c[12];
+        load_tri_rgba<12>(fp.src.rgba, t, c);
         cr = c[0] + (c[4] - c[0]) * w1 + (c[8] - c[0]) * w2;
         cg = c[1] + (c[5] - c[1]) * w1 + (c[9] - c[1]) * w2;
         cb = c[2] + (c[6] - c[2]) * w1 + (c[10] - c[2]) * w2;
         ca = c[3] + (c[7] - c[3]) * w1 + (c[11] - c[3]) * w2;
     } else {
-        const f64* c = fp.src.rgba + t * 4;
+        f64 c[4];
+        load_tri_rgba<4>(fp.src.rgba, t, c);
         cr = c[0]; cg = c[1]; cb = c[2]; ca = c[3];
     }
     // ApplyPixel (cpp:529-547); ca * ct3 == 1 for every batch routed here
@@ -338,9 +350,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
             const u32 b = ls + c * 64 + lane;
             if (c < nch && b < le) {
                 pt = list[b];
-                const f64* q = fp.src.xy + (i64)pt * 6;
-#pragma unroll
-                for (int v = 0; v < 6; ++v) pxy[v] = q[v];
+                load_tri_xy(fp.src.xy, pt, pxy);
                 if (DEPTH && fp.src.z) {
                     const f64* qz = fp.src.z + (i64)pt * 3;
                     pz[0] = qz[0]; pz[1] = qz[1]; pz[2] = qz[2];
@@ -545,6 +555,9 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         sc.fitems = ib[0];
         return ok;
     };
+    u64* rb[1] = {sc.frect};
+    if (!grow_set(rb, &sc.frect_cap, (size_t)src.n)) return false;
+    sc.frect = rb[0];
     size_t cap;
     if (!exact) {
         const u64 est = std::max<u64>(std::max<u64>(sc.lastPairs + sc.lastPairs / 4, (u64)src.n * 2), 1u << 20);
@@ -565,8 +578,8 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     u32 grid;
     for (int attempt = 0;; ++attempt) {
         nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
-        if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.fcnt, ntiles);
-        else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, s, bp, sc.fcnt, ntiles);
+        if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.fcnt, ntiles, sc.frect);
+        else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, s, bp, sc.fcnt, ntiles, sc.frect);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
 
@@ -597,8 +610,8 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     }
 
     nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
-    if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.dplan);
-    else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.dplan);
+    if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.frect, sc.dplan);
+    else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.frect, sc.dplan);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
 

@@ -248,6 +248,18 @@ class RenderContext:
             zp = _f64_ptr(z)
         lib.DrawTriangles(self._ptr, _f64_ptr(xy), zp, _f64_ptr(rgba), n, bool(gouraud))
 
+    def draw_triangles_device(self, xy, rgba, n: int, z=None, gouraud: bool = False):
+        """DrawTrianglesDevice: the arrays already live in HBM on this
+        context's device.  xy / rgba / z are device addresses (int) or objects
+        with .data_ptr() (e.g. torch tensors, contiguous f64); layouts as
+        draw_triangles.  The call only enqueues work: keep the arrays alive
+        until the next sync point (flush / any readback)."""
+        def addr(a):
+            if a is None:
+                return None
+            return a.data_ptr() if hasattr(a, "data_ptr") else int(a)
+        lib.DrawTrianglesDevice(self._ptr, addr(xy), addr(z), addr(rgba), int(n), bool(gouraud))
+
     def draw_triangle_buffer(self, buf: "TriangleBuffer"):
         lib.DrawTriangleBuffer(self._ptr, buf._ptr)
 

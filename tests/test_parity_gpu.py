@@ -105,6 +105,31 @@ def test_triangle_buffer_equals_host_arrays(gpu):
     assert_same(a, {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, "buffer")
 
 
+@pytest.mark.parametrize("misalign", [False, True])
+def test_device_arrays_match_oracle(gpu, oracle, misalign):
+    """DrawTrianglesDevice on torch HBM tensors, 16-byte aligned or not
+    (misaligned arrays are re-staged: the kernels load 16-byte vectors)."""
+    import torch
+    xy, z, c = scenes.triangle_soup(5000, 500, 300, 15, seed=19, gouraud=True)
+    a, _ = _tri_frame(oracle, 500, 300, xy, z, c)
+    o = 1 if misalign else 0
+
+    def dev(arr):
+        flat = np.ascontiguousarray(arr, np.float64).ravel()
+        t = torch.zeros(flat.size + o, dtype=torch.float64, device="cuda")
+        t[o:] = torch.from_numpy(flat).to("cuda")
+        return t[o:]
+    dxy, dz, dc = dev(xy), dev(z), dev(c)
+    assert (dxy.data_ptr() % 16 != 0) == misalign
+    torch.cuda.synchronize()
+    ctx = gpu.context(500, 300, False)
+    ctx.set_color(0, 0, 0, 0)
+    ctx.set_depth_state(True, True)
+    ctx.clear_depth()
+    ctx.draw_triangles_device(dxy, dc, len(xy), z=dz, gouraud=True)
+    assert_same(a, {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, "device")
+
+
 def test_c3_order_independent_depth_full_size(gpu):
     """Size-independent property at full C3 size: with LESS + write the depth
     buffer is min(clear, min zq) whatever the submission order."""
