@@ -104,50 +104,75 @@ __device__ __forceinline__ u32 tile_items(u32 c, bool owned) {
     return owned ? (c > SLICE ? (c + SLICE - 1) / SLICE : 1u) : 0u;
 }
 
-__global__ __launch_bounds__(1024) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int nshards,
-                                                    int shard, u32* __restrict__ off, uint4* __restrict__ items,
-                                                    u32* __restrict__ cur, u32* __restrict__ totals,
-                                                    u32* __restrict__ host_totals, u32 cap, u32 icap) {
-    __shared__ u32 sA[1024], sB[1024], sC[1024];
-    const int tid = threadIdx.x;
-    const int per = (ntiles + 1023) / 1024;
-    const int b0 = tid * per, b1 = min(b0 + per, ntiles);
+// Inclusive wave scan (64 lanes).
+__device__ __forceinline__ u32 wave_scan(u32 v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+constexpr int PLAN_T = 1024, PLAN_W = PLAN_T / 64;
+
+// Tiles are taken PLAN_T at a time (thread = tile: coalesced), each round a
+// workgroup scan carried over from the previous one.
+__global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int nshards,
+                                                      int shard, u32* __restrict__ off, uint4* __restrict__ items,
+                                                      u32* __restrict__ cur, u32* __restrict__ totals,
+                                                      u32* __restrict__ host_totals, u32 cap, u32 icap) {
+    __shared__ u32 sh[3][PLAN_W];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // pass 1: totals (the capacity check needs them before any item is written)
     u32 a = 0, b = 0, m = 0;
-    for (int i = b0; i < b1; ++i) {
+    for (int i = tid; i < ntiles; i += PLAN_T) {
         const u32 c = cnt[i];
         a += c;
         b += tile_items(c, owned_row(i / tiles_x, nshards, shard));
         m += c > SLICE ? 1u : 0u;
     }
-    sA[tid] = a; sB[tid] = b; sC[tid] = m;
+    a = wave_scan(a, lane); b = wave_scan(b, lane); m = wave_scan(m, lane);
+    if (lane == 63) { sh[0][w] = a; sh[1][w] = b; sh[2][w] = m; }
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const u32 va = tid >= d ? sA[tid - d] : 0u;
-        const u32 vb = tid >= d ? sB[tid - d] : 0u;
-        const u32 vc = tid >= d ? sC[tid - d] : 0u;
+    u32 ta = 0, tb = 0, tm = 0;
+#pragma unroll
+    for (int k = 0; k < PLAN_W; ++k) { ta += sh[0][k]; tb += sh[1][k]; tm += sh[2][k]; }
+    const bool fits = ta <= cap && tb <= icap;
+    __syncthreads();
+    // pass 2: offsets and items
+    u32 carryA = 0, carryB = 0;
+    for (int r0 = 0; r0 < ntiles; r0 += PLAN_T) {
+        const int i = r0 + tid;
+        u32 c = 0, ni = 0;
+        if (i < ntiles) {
+            c = cnt[i];
+            ni = tile_items(c, owned_row(i / tiles_x, nshards, shard));
+        }
+        const u32 ia = wave_scan(c, lane), ib = wave_scan(ni, lane);
+        if (lane == 63) { sh[0][w] = ia; sh[1][w] = ib; }
         __syncthreads();
-        sA[tid] += va; sB[tid] += vb; sC[tid] += vc;
+        u32 ea = carryA + ia - c, eb = carryB + ib - ni;
+#pragma unroll
+        for (int k = 0; k < PLAN_W; ++k) {
+            if (k < w) { ea += sh[0][k]; eb += sh[1][k]; }
+            carryA += sh[0][k]; carryB += sh[1][k];
+        }
         __syncthreads();
+        if (i < ntiles) {
+            off[i] = ea;
+            if (fits)
+                for (u32 k = 0; k < ni; ++k) {
+                    const u32 ls = ea + k * SLICE;
+                    items[eb + k] = make_uint4((u32)i, ls, min(ls + SLICE, ea + c), ni);
+                }
+            cnt[i] = 0;
+            cur[i] = 0;
+        }
     }
-    const bool fits = sA[1023] <= cap && sB[1023] <= icap;
-    u32 ea = sA[tid] - a, eb = sB[tid] - b;
-    for (int i = b0; i < b1; ++i) {
-        const u32 c = cnt[i];
-        off[i] = ea;
-        const u32 ni = tile_items(c, owned_row(i / tiles_x, nshards, shard));
-        if (fits)
-            for (u32 k = 0; k < ni; ++k) {
-                const u32 ls = ea + k * SLICE;
-                items[eb + k] = make_uint4((u32)i, ls, min(ls + SLICE, ea + c), ni);
-            }
-        ea += c;
-        eb += ni;
-        cnt[i] = 0;
-        cur[i] = 0;
-    }
-    if (tid == 1023) {
-        off[ntiles] = sA[1023];
-        const u32 t[4] = {sA[1023], sB[1023], sC[1023], fits ? 1u : 0u};
+    if (tid == 0) {
+        off[ntiles] = ta;
+        const u32 t[4] = {ta, tb, tm, fits ? 1u : 0u};
         for (int k = 0; k < 4; ++k) {
             totals[k] = t[k];
             __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1,6 +1,7 @@
 # rocprofv3 runs of bench.py: one kernel-trace --stats pass, then PMC passes
 # (each counter group in its own run, kernel-trace only beside --pmc), all
 # restricted to the dominant kernel.  Usage: bash tools/profile.sh <config> <tag>
+# (PMC=0: the kernel trace only)
 cd $GRAFT_REPO_ROOT
 CFG=${1:-c3}
 TAG=${2:-r01}
@@ -18,6 +19,7 @@ run() {  # name, timeout, args...
 run list 60 rocprofv3 -L
 grep -oE "^[[:space:]]*(SQ_|TCC_|TCP_|GRBM_|FETCH|WRITE)[A-Za-z0-9_]*" $OUT/list.log | sort -u > $OUT/counter_names.txt
 run trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $BENCH --steps 10 --warmup 2
+[ "${PMC:-1}" = 1 ] || { ls -R $OUT | head -20; exit 0; }
 KR=${KERNEL_REGEX:-"k_vis|k_resolve|k_tile_raster"}
 run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_fetch -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
 run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_write -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
