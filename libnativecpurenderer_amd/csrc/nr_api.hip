@@ -232,8 +232,10 @@ static hipEvent_t ev_get(RenderContext* ctx) {
         ctx->evPool.pop_back();
         return e;
     }
+    // timing only: no system-scope fence at record (a fenced record leaves a
+    // multi-microsecond bubble between the kernels it separates)
     hipEvent_t e;
-    NR_CHECK(hipEventCreate(&e));
+    NR_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     return e;
 }
 
@@ -326,7 +328,6 @@ void DestroyRenderContext(RenderContext* ctx) {
         if (p) NR_CHECK(hipFree(p));
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));
     if (t.h_plan) NR_CHECK(hipHostFree(t.h_plan));
-    if (t.planEvent) NR_CHECK(hipEventDestroy(t.planEvent));
     for (auto& p : ctx->evPending) {
         NR_CHECK(hipEventDestroy(p.second.first));
         NR_CHECK(hipEventDestroy(p.second.second));

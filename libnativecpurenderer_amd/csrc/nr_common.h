@@ -52,7 +52,7 @@ struct TriScratch {
     u32* dplan = nullptr;
     u32* h_plan = nullptr;                  // pinned, device-mapped copy of the plan totals
     u32* d_hplan = nullptr;                 // its device address
-    hipEvent_t planEvent = nullptr;
+    u32 planSeq = 0;                        // sequence number of the last async plan
     u64 lastPairs = 0;                      // capacity estimate for the next batch
     u64 capOverride = 0;                    // testing: force this pair capacity
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays

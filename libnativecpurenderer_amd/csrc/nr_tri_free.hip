@@ -29,6 +29,8 @@
 //                    it and resets those keys.
 #include "nr_tri.h"
 
+#include <thread>
+
 namespace nrtri {
 namespace {
 
@@ -121,7 +123,7 @@ constexpr int PLAN_T = 1024, PLAN_W = PLAN_T / 64;
 __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int nshards,
                                                       int shard, u32* __restrict__ off, uint4* __restrict__ items,
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
-                                                      u32* __restrict__ host_totals, u32 cap, u32 icap) {
+                                                      u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq) {
     __shared__ u32 sh[3][PLAN_W];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // pass 1: totals (the capacity check needs them before any item is written)
@@ -177,6 +179,8 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
             totals[k] = t[k];
             __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        // the batch's sequence number last: the host polls it (nr_settle)
+        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -553,7 +557,8 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     }
     if (!sc.dplan) NR_CHECK(hipMalloc(&sc.dplan, 4 * sizeof(u32)));
     if (!sc.h_plan) {
-        NR_CHECK(hipHostMalloc((void**)&sc.h_plan, 4 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
+        NR_CHECK(hipHostMalloc((void**)&sc.h_plan, 8 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
+        sc.h_plan[4] = 0;
         NR_CHECK(hipHostGetDevicePointer((void**)&sc.d_hplan, sc.h_plan, 0));
     }
     u64* vb[1] = {sc.vis};
@@ -611,13 +616,11 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
         hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, fp.tiles_x, fp.nshards,
                            fp.shard, sc.foff, sc.fitems, sc.fcur, sc.dplan, sc.d_hplan, (u32)cap,
-                           (u32)std::min<size_t>(sc.fitems_cap, 0xFFFFFFF0ull));
+                           (u32)std::min<size_t>(sc.fitems_cap, 0xFFFFFFF0ull), ++sc.planSeq);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
 
         if (!exact) {
-            if (!sc.planEvent) NR_CHECK(hipEventCreateWithFlags(&sc.planEvent, hipEventDisableTiming));
-            NR_CHECK(hipEventRecord(sc.planEvent, s));
             grid = (u32)std::min<u64>(sc.fitems_cap, 8192);   // grid-stride over the items
             break;
         }
@@ -685,7 +688,22 @@ void settle(RenderContext* ctx) {
     if (!pb) return;
     ctx->pendingBatch = nullptr;
     TriScratch& sc = ctx->tri;
-    NR_CHECK(hipEventSynchronize(sc.planEvent));
+    // wait for the batch's plan (usually long finished): it writes its
+    // sequence number into pinned host memory after the totals -- polling it
+    // avoids an event record per batch (each costs a multi-microsecond
+    // bubble on the stream)
+    const u32 want = sc.planSeq;
+    for (u64 spin = 0; __atomic_load_n(&sc.h_plan[4], __ATOMIC_ACQUIRE) != want; ++spin) {
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(ctx->stream);
+            if (q != hipErrorNotReady && __atomic_load_n(&sc.h_plan[4], __ATOMIC_ACQUIRE) != want) {
+                nr_set_error_msg("triangle batch: plan result missing (stream idle or failed)");
+                delete pb;
+                return;
+            }
+            std::this_thread::yield();
+        }
+    }
     if (sc.h_plan[3]) {
         sc.lastPairs = sc.h_plan[0];
     } else {
