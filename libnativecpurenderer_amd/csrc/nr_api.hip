@@ -688,9 +688,12 @@ void ResolvePending(RenderContext* ctx) {
 void* GetDeviceBufferPtr(RenderContext* ctx) { return ctx->buffer; }
 void* GetStreamPtr(RenderContext* ctx) { return (void*)ctx->stream; }
 
+// Switching off does not synchronise: recorded pairs are read at the next
+// GetKernelTiming (or once 4096 are pending), so timing can be toggled per
+// frame inside a timed loop.
 void EnableKernelTiming(RenderContext* ctx, bool on) {
     ctx->timing = on;
-    if (!on) timing_collect(ctx);
+    if (ctx->evPending.size() >= 4096) timing_collect(ctx);
 }
 
 // Sum and count of the named kernel's durations since the last reset

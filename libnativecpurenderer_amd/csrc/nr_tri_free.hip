@@ -304,6 +304,7 @@ __device__ __forceinline__ void resolve_pixel(const FrameParams& fp, i64 px, i64
 
 enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
 constexpr int NW = VWG / 64;   // waves per k_vis workgroup
+constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 
 // Wave-synchronous ordering of this wave's own LDS traffic (a wave's LDS
 // operations complete in order; this stops the compiler from reordering them).
@@ -325,8 +326,10 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
                                              u64* __restrict__ vis, u32* __restrict__ done,
                                              const u32* __restrict__ plan) {
     constexpr bool DEPTH = ZMODE != 0;
-    __shared__ u64 key[TH * TW];
-    __shared__ u32 zin[ZMODE == 2 ? TH * TW : 1];
+    // tile keys, rows padded to KS = 65 entries: lanes working on different
+    // rows at the same column then hit different LDS banks
+    __shared__ u64 key[TH * KS];
+    __shared__ u32 zin[ZMODE == 2 ? TH * KS : 1];
     __shared__ f64 S[NW][F_NSLOT][64];
     __shared__ iu8 MAP[NW][64 * TH];
     __shared__ iu8 RR0[NW][64];
@@ -366,8 +369,8 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
             u32 z0 = 0xFFFFFFFFu;
             if (DEPTH && lx < wlim && ly < hlim)
                 z0 = fp.pendDepth ? fp.pendDepthValue : fp.depth[(y0 + ly) * fp.W + x0 + lx];
-            key[p] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
-            if (ZMODE == 2) zin[p] = z0;
+            key[ly * KS + lx] = ZMODE == 1 ? ((u64)z0 << 32) : 0ull;
+            if (ZMODE == 2) zin[ly * KS + lx] = z0;
         }
         __syncthreads();
 
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
                 const u64 id1 = TT[wave][k];
                 if (ZMODE == 0) {
 #pragma clang loop vectorize(disable) interleave(disable)
-                    for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * TW + lx], id1);
+                    for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * KS + lx], id1);
                     continue;
                 }
                 const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
                     const f64 w2 = (e1x * dy - dx * e1y) * inv;
                     const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
                     const u32 zq = nr_quantize_depth_bl(zz);
-                    const int p = r * TW + lx;
+                    const int p = r * KS + lx;
                     if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
                     else if (zq < zin[p]) atomicMax(&key[p], id1);
                 }
@@ -472,7 +475,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         if (!multi) {   // the whole list was in this slice: shade now
             for (int p = tid; p < TH * TW; p += VWG) {
                 const int lx = p & (TW - 1), ly = p / TW;
-                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[p]);
+                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[ly * KS + lx]);
             }
             continue;
         }
@@ -486,8 +489,8 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
             const int lx = p & (TW - 1), ly = p / TW;
             if (lx >= wlim || ly >= hlim) continue;
             u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-            if (ZMODE == 1) atomicMin(g, key[p]);
-            else atomicMax(g, key[p]);
+            if (ZMODE == 1) atomicMin(g, key[ly * KS + lx]);
+            else atomicMax(g, key[ly * KS + lx]);
         }
         __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: this wave's atomics performed
         __syncthreads();

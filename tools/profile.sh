@@ -25,5 +25,6 @@ run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -d $OU
 run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" -d $OUT/pmc_write -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
 run pmc_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-include-regex "$KR" -d $OUT/pmc_sq1 -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
 run pmc_sq2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex "$KR" -d $OUT/pmc_sq2 -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
+run pmc_sq3 300 rocprofv3 --pmc SQ_LEVEL_WAVES SQ_INSTS_LDS_ATOMIC SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_THREAD_CYCLES_VALU --kernel-include-regex "$KR" -d $OUT/pmc_sq3 -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
 run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KR" -d $OUT/pmc_tcc -o run --output-format csv -- python3 $BENCH --steps 3 --warmup 1
 ls -R $OUT | head -50
