@@ -117,6 +117,19 @@ __device__ __forceinline__ u32 wave_scan(u32 v, int lane) {
 }
 
 constexpr int PLAN_T = 1024, PLAN_W = PLAN_T / 64;
+constexpr int PLAN_NB = 12;
+
+// Size class of a tile's work items: 0 empty, 1 + floor(log2(count)) (capped)
+// for one slice, PLAN_NB - 1 for tiles split over several slices.  Items are
+// laid out largest class first: k_vis workgroups take items in index order,
+// so the long ones start first and the short ones fill the tail (a longest-
+// first schedule).  Results do not depend on the order (order-free raster).
+__device__ __forceinline__ int size_class(u32 c) {
+    if (c > SLICE) return PLAN_NB - 1;
+    if (c == 0) return 0;
+    const int l = 31 - __clz(c);
+    return 1 + (l < PLAN_NB - 3 ? l : PLAN_NB - 3);
+}
 
 // Tiles are taken PLAN_T at a time (thread = tile: coalesced), each round a
 // workgroup scan carried over from the previous one.
@@ -125,14 +138,20 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
                                                       u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq) {
     __shared__ u32 sh[3][PLAN_W];
+    __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    // pass 1: totals (the capacity check needs them before any item is written)
+    if (tid < PLAN_NB) bcnt[tid] = 0;
+    __syncthreads();
+    // pass 1: totals (the capacity check needs them before any item is
+    // written) and the number of items per size class
     u32 a = 0, b = 0, m = 0;
     for (int i = tid; i < ntiles; i += PLAN_T) {
         const u32 c = cnt[i];
+        const u32 ni = tile_items(c, owned_row(i / tiles_x, nshards, shard));
         a += c;
-        b += tile_items(c, owned_row(i / tiles_x, nshards, shard));
+        b += ni;
         m += c > SLICE ? 1u : 0u;
+        if (ni) atomicAdd(&bcnt[size_class(c)], ni);
     }
     a = wave_scan(a, lane); b = wave_scan(b, lane); m = wave_scan(m, lane);
     if (lane == 63) { sh[0][w] = a; sh[1][w] = b; sh[2][w] = m; }
@@ -141,9 +160,13 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
 #pragma unroll
     for (int k = 0; k < PLAN_W; ++k) { ta += sh[0][k]; tb += sh[1][k]; tm += sh[2][k]; }
     const bool fits = ta <= cap && tb <= icap;
+    if (tid == 0) {   // item ranges of the classes, largest class first
+        u32 base = 0;
+        for (int k = PLAN_NB - 1; k >= 0; --k) { bcur[k] = base; base += bcnt[k]; }
+    }
     __syncthreads();
     // pass 2: offsets and items
-    u32 carryA = 0, carryB = 0;
+    u32 carryA = 0;
     for (int r0 = 0; r0 < ntiles; r0 += PLAN_T) {
         const int i = r0 + tid;
         u32 c = 0, ni = 0;
@@ -151,23 +174,25 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
             c = cnt[i];
             ni = tile_items(c, owned_row(i / tiles_x, nshards, shard));
         }
-        const u32 ia = wave_scan(c, lane), ib = wave_scan(ni, lane);
-        if (lane == 63) { sh[0][w] = ia; sh[1][w] = ib; }
+        const u32 ia = wave_scan(c, lane);
+        if (lane == 63) sh[0][w] = ia;
         __syncthreads();
-        u32 ea = carryA + ia - c, eb = carryB + ib - ni;
+        u32 ea = carryA + ia - c;
 #pragma unroll
         for (int k = 0; k < PLAN_W; ++k) {
-            if (k < w) { ea += sh[0][k]; eb += sh[1][k]; }
-            carryA += sh[0][k]; carryB += sh[1][k];
+            if (k < w) ea += sh[0][k];
+            carryA += sh[0][k];
         }
         __syncthreads();
         if (i < ntiles) {
             off[i] = ea;
-            if (fits)
+            if (fits && ni) {
+                const u32 eb = atomicAdd(&bcur[size_class(c)], ni);
                 for (u32 k = 0; k < ni; ++k) {
                     const u32 ls = ea + k * SLICE;
                     items[eb + k] = make_uint4((u32)i, ls, min(ls + SLICE, ea + c), ni);
                 }
+            }
             cnt[i] = 0;
             cur[i] = 0;
         }
