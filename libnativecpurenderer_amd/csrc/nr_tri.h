@@ -157,6 +157,58 @@ __device__ __forceinline__ void row_span_in(const f64 (&sx)[3], const f64 (&sy)[
     if (xe < xs) xe = xs;
 }
 
+// Edge slopes for row_span_slopes, one per pointInPolygon edge (i, j) in its
+// orientation: e0 = (0,2), e1 = (1,0), e2 = (2,1); slope = (sx[j]-sx[i]) /
+// (sy[j]-sy[i]) (inf/NaN for a horizontal edge, which never straddles a row).
+__device__ __forceinline__ void edge_slopes(const f64 (&sx)[3], const f64 (&sy)[3], f64 (&sl)[3]) {
+    sl[0] = (sx[2] - sx[0]) / (sy[2] - sy[0]);
+    sl[1] = (sx[0] - sx[1]) / (sy[0] - sy[1]);
+    sl[2] = (sx[1] - sx[2]) / (sy[1] - sy[2]);
+}
+
+// One crossing without a division.  The exact crossing is
+//   cc  = fl(fl(fl(a*b) / d) + c)      a = sx[j]-sx[i], b = y-sy[i], d = sy[j]-sy[i], c = sx[i]
+// and with the per-edge slope s = fl(a/d):
+//   cc' = fl(fl(b*s) + c).
+// With unit roundoff u = 2^-53 both products are A(1+e)(1+e') for A = a*b/d,
+// so |fl(a*b)/d - fl(b*s)| <= (4u + 2u^2)|A|, and the two final roundings add
+// u|cc| + u|cc'|; hence |cc - cc'| <= 4.001u|v| + 2.001u|cc'| (v = fl(b*s))
+// < 2^-50 (|v| + |cc'|) = eps (plus 2^-1000 for underflow).  ceil is what the
+// span needs: if cc' is more than eps away from the integers on both sides of
+// it, ceil(cc) == ceil(cc').  The lane reports `safe`; otherwise the caller
+// evaluates the exact expression (integer-aligned vertices hit that path,
+// arbitrary geometry essentially never).
+__device__ __forceinline__ f64 crossing_ceil(f64 b, f64 s, f64 c, bool& safe) {
+    const f64 v = b * s;
+    const f64 cc = v + c;
+    const f64 k = ceil(cc);
+    const f64 eps = (fabs(v) + fabs(cc)) * 0x1p-50 + 0x1p-1000;
+    safe = safe && (cc - (k - 1.0) > eps) && (k - cc > eps);
+    return k;
+}
+
+// row_span_in with the per-edge slopes (no division unless a crossing lies
+// within eps of an integer, see crossing_ceil): the same [xs, xe).
+__device__ __forceinline__ void row_span_slopes(const f64 (&sx)[3], const f64 (&sy)[3], const f64 (&sl)[3], f64 y,
+                                                f64 x0, f64 wlim, int& xs, int& xe) {
+    const bool b0 = sy[0] > y, b1 = sy[1] > y, b2 = sy[2] > y;
+    const bool v1 = (b1 != b0) && (b1 != b2);
+    const bool v2 = (b2 != b0) && (b2 != b1);
+    const f64 aix = v1 ? sx[2] : sx[0], aiy = v1 ? sy[2] : sy[0], sa = v1 ? sl[2] : sl[0];
+    const f64 bix = v2 ? sx[2] : sx[1], biy = v2 ? sy[2] : sy[1], sb = v2 ? sl[2] : sl[1];
+    bool safe = true;
+    f64 ka = crossing_ceil(y - aiy, sa, aix, safe);
+    f64 kb = crossing_ceil(y - biy, sb, bix, safe);
+    if (!safe) {   // exact expression (cpp:832-839 order of operations)
+        const f64 ajx = v1 ? sx[1] : sx[2], ajy = v1 ? sy[1] : sy[2];
+        const f64 bjx = v2 ? sx[1] : sx[0], bjy = v2 ? sy[1] : sy[0];
+        ka = ceil((ajx - aix) * (y - aiy) / (ajy - aiy) + aix);
+        kb = ceil((bjx - bix) * (y - biy) / (bjy - biy) + bix);
+    }
+    xs = (int)clampd(fmin(ka, kb) - x0, 0.0, wlim);
+    xe = (int)clampd(fmax(ka, kb) - x0, 0.0, wlim);
+}
+
 // State snapshot of one draw call (passed by value to the kernels).
 struct FrameParams {
     TriSrc src;

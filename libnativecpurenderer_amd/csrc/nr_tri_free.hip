@@ -257,74 +257,187 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
     }
 }
 
-// Deferred shading of one pixel from its packed visibility key (id1 = 0: no
-// fragment won; the pending clears still land).  Winner: barycentrics ->
-// colour -> ApplyPixel -> framebuffer (+ u8 frame) and depth written once.
-template <int ZMODE, bool GOURAUD>
-__device__ __forceinline__ void resolve_pixel(const FrameParams& fp, i64 px, i64 py, u64 kv) {
-    const i64 p = py * fp.W + px;
+// ---- deferred shading --------------------------------------------------
+// A workgroup shades its tile after the raster.  The winners of the tile's
+// pixels are few (a triangle wins ~9 pixels of the C3 mesh), so they are
+// de-duplicated in an LDS hash table, each distinct winner's data is fetched
+// once (one round of independent global loads, one thread per winner) and
+// turned into a shading record in LDS, and the pixels are then shaded from
+// LDS.  Per-pixel dependent global loads (eight rounds of latency per
+// thread) were the largest cost of the fused raster.
+constexpr int HTS = 512;    // hash slots (power of two)
+constexpr int RMAX = 256;   // staged winner records per tile; later winners load directly
+constexpr int MAXPROBE = 16;   // linear-probe limit: a winner not placed / found within it loads directly
+
+template <bool GOURAUD>
+struct ShadeStage {
+    // Gouraud record: sx0 sy0 e1x e1y e2x e2y inv | c0 rgb | (c1-c0) rgb | (c2-c0) rgb
+    // flat record: rgb.  Alpha is not staged: every batch routed here has
+    // vertex alpha 1 (and colourTransform[3] == 1), so the interpolated alpha
+    // is 1 + 0*w1 + 0*w2, computed as such.
+    static constexpr int REC = GOURAUD ? 16 : 3;
+    static constexpr int HT = 0, HIDX = HTS * 4, DIDX = HTS * 6, REC_OFF = ((HTS * 6 + RMAX * 4) + 15) & ~15;
+    static constexpr int BYTES = REC_OFF + RMAX * REC * 8;
+};
+
+__device__ __forceinline__ u32 ht_hash(u32 id) { return (id * 2654435761u) >> 23; }   // 9 bits = HTS
+
+// Pending clears for a pixel no fragment won.
+template <int ZMODE>
+__device__ __forceinline__ void store_clear(const FrameParams& fp, i64 p) {
+    if (fp.pendColor) {
+        const int ipp = fp.ipp;
+        f64* dst = fp.fb + p * ipp;
+        const f64 v = fp.pendColorValue;
+        dst[0] = v; dst[1] = v; dst[2] = v;
+        if (ipp == 4) dst[3] = v;
+        if (fp.frameU8) {
+            iu8* d8 = fp.frameU8 + p * ipp;
+            const iu8 v8 = nr_to_u8(v);
+            d8[0] = v8; d8[1] = v8; d8[2] = v8;
+            if (ipp == 4) d8[3] = v8;
+        }
+    }
+    if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+}
+
+// ApplyPixel (cpp:529-547) of the winner's colour, then framebuffer (+ u8
+// frame) and depth written once.  ca == 1 except for non-finite
+// barycentrics; the destination is read only then.
+template <int ZMODE>
+__device__ __forceinline__ void store_pixel(const FrameParams& fp, i64 p, u64 kv, f64 cr, f64 cg, f64 cb, f64 ca) {
     const int ipp = fp.ipp;
     f64* dst = fp.fb + p * ipp;
-    iu8* d8 = fp.frameU8 ? fp.frameU8 + p * ipp : nullptr;
-    const u32 id1 = (u32)kv;
-    if (id1 == 0) {
-        if (fp.pendColor) {
-            const f64 v = fp.pendColorValue;
-            dst[0] = v; dst[1] = v; dst[2] = v;
-            if (ipp == 4) dst[3] = v;
-            if (d8) {
-                const iu8 v8 = nr_to_u8(v);
-                d8[0] = v8; d8[1] = v8; d8[2] = v8;
-                if (ipp == 4) d8[3] = v8;
-            }
-        }
-        if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
-        return;
-    }
-    f64 R, G, B, A = 0;
-    if (fp.pendColor) {
-        R = G = B = A = fp.pendColorValue;
-    } else {
-        R = dst[0]; G = dst[1]; B = dst[2];
-        if (ipp == 4) A = dst[3];
-    }
-    (void)A;
-    const i64 t = (i64)id1 - 1;
-    f64 cr, cg, cb, ca;
-    if (GOURAUD) {
-        f64 sx[3], sy[3];
-        tri_screen(fp.src, fp.m, t, sx, sy);
-        const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-        const f64 inv = 1.0 / (e1x * e2y - e2x * e1y);
-        const f64 dx = (f64)px - sx[0], dy = (f64)py - sy[0];
-        const f64 w1 = (dx * e2y - e2x * dy) * inv;
-        const f64 w2 = (e1x * dy - dx * e1y) * inv;
-        f64 c[12];
-        load_tri_rgba<12>(fp.src.rgba, t, c);
-        cr = c[0] + (c[4] - c[0]) * w1 + (c[8] - c[0]) * w2;
-        cg = c[1] + (c[5] - c[1]) * w1 + (c[9] - c[1]) * w2;
-        cb = c[2] + (c[6] - c[2]) * w1 + (c[10] - c[2]) * w2;
-        ca = c[3] + (c[7] - c[3]) * w1 + (c[11] - c[3]) * w2;
-    } else {
-        f64 c[4];
-        load_tri_rgba<4>(fp.src.rgba, t, c);
-        cr = c[0]; cg = c[1]; cb = c[2]; ca = c[3];
-    }
-    // ApplyPixel (cpp:529-547); ca * ct3 == 1 for every batch routed here
     cr *= fp.ct[0]; cg *= fp.ct[1]; cb *= fp.ct[2]; ca *= fp.ct[3];
     if (ca != 1) {
+        f64 R, G, B;
+        if (fp.pendColor) {
+            R = G = B = fp.pendColorValue;
+        } else {
+            R = dst[0]; G = dst[1]; B = dst[2];
+        }
         cr = R * (1 - ca) + cr * ca;
         cg = G * (1 - ca) + cg * ca;
         cb = B * (1 - ca) + cb * ca;
     }
     dst[0] = cr; dst[1] = cg; dst[2] = cb;
     if (ipp == 4) dst[3] = ca;
-    if (d8) {
+    if (fp.frameU8) {
+        iu8* d8 = fp.frameU8 + p * ipp;
         d8[0] = nr_to_u8(cr); d8[1] = nr_to_u8(cg); d8[2] = nr_to_u8(cb);
         if (ipp == 4) d8[3] = nr_to_u8(ca);
     }
     if (ZMODE == 1) fp.depth[p] = (u32)(kv >> 32);
     else if (ZMODE == 2 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+}
+
+// Shading record of triangle t (the expressions of the per-pixel path, once).
+template <bool GOURAUD>
+__device__ __forceinline__ void make_record(const FrameParams& fp, i64 t, f64* r) {
+    if (GOURAUD) {
+        f64 sx[3], sy[3];
+        tri_screen(fp.src, fp.m, t, sx, sy);
+        f64 c[12];
+        load_tri_rgba<12>(fp.src.rgba, t, c);
+        const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+        r[0] = sx[0]; r[1] = sy[0]; r[2] = e1x; r[3] = e1y; r[4] = e2x; r[5] = e2y;
+        r[6] = 1.0 / (e1x * e2y - e2x * e1y);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            r[7 + k] = c[k];
+            r[10 + k] = c[4 + k] - c[k];
+            r[13 + k] = c[8 + k] - c[k];
+        }
+    } else {
+        f64 c[4];
+        load_tri_rgba<4>(fp.src.rgba, t, c);
+        r[0] = c[0]; r[1] = c[1]; r[2] = c[2];
+    }
+}
+
+// Colour of pixel (px, py) from a record.
+template <bool GOURAUD>
+__device__ __forceinline__ void record_colour(const f64* r, i64 px, i64 py, f64& cr, f64& cg, f64& cb, f64& ca) {
+    if (GOURAUD) {
+        const f64 dx = (f64)px - r[0], dy = (f64)py - r[1];
+        const f64 w1 = (dx * r[5] - r[4] * dy) * r[6];
+        const f64 w2 = (r[2] * dy - dx * r[3]) * r[6];
+        cr = r[7] + r[10] * w1 + r[13] * w2;
+        cg = r[8] + r[11] * w1 + r[14] * w2;
+        cb = r[9] + r[12] * w1 + r[15] * w2;
+        ca = 1.0 + 0.0 * w1 + 0.0 * w2;   // c[3] + (c[7]-c[3])*w1 + (c[11]-c[3])*w2 with unit alphas
+    } else {
+        cr = r[0]; cg = r[1]; cb = r[2]; ca = 1.0;
+    }
+}
+
+// Shades the tile from its LDS keys (key(p) for tile pixel p = ly*TW + lx).
+template <int ZMODE, bool GOURAUD, int NT, typename KeyFn>
+__device__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int hlim, KeyFn key, unsigned char* smem,
+                           u32& nU) {
+    using St = ShadeStage<GOURAUD>;
+    u32* ht = reinterpret_cast<u32*>(smem + St::HT);
+    unsigned short* hidx = reinterpret_cast<unsigned short*>(smem + St::HIDX);
+    u32* didx = reinterpret_cast<u32*>(smem + St::DIDX);
+    f64* rec = reinterpret_cast<f64*>(smem + St::REC_OFF);
+    const int tid = threadIdx.x;
+    auto valid = [&](int p) { return (p & (TW - 1)) < wlim && p / TW < hlim; };
+    for (int i = tid; i < HTS; i += NT) ht[i] = 0;
+    if (tid == 0) nU = 0;
+    __syncthreads();
+    // distinct winners -> dense indices
+    for (int p = tid; p < TH * TW; p += NT) {
+        if (!valid(p)) continue;
+        const u32 id = (u32)key(p);
+        if (!id) continue;
+        u32 h = ht_hash(id);
+        for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
+            const u32 cur = ht[h];
+            if (cur == id) break;
+            if (cur == 0) {
+                const u32 old = atomicCAS(&ht[h], 0u, id);
+                if (old == 0) {
+                    const u32 d = atomicAdd(&nU, 1u);
+                    hidx[h] = (unsigned short)(d < RMAX ? d : RMAX);
+                    if (d < RMAX) didx[d] = id;
+                    break;
+                }
+                if (old == id) break;
+            }
+        }
+    }
+    __syncthreads();
+    // one record per staged winner (independent loads: one latency round)
+    const u32 U = nU < (u32)RMAX ? nU : (u32)RMAX;
+    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);
+    __syncthreads();
+    for (int p = tid; p < TH * TW; p += NT) {
+        if (!valid(p)) continue;
+        const i64 px = x0 + (p & (TW - 1)), py = y0 + p / TW;
+        const i64 gp = py * fp.W + px;
+        const u64 kv = key(p);
+        const u32 id = (u32)kv;
+        if (!id) {
+            store_clear<ZMODE>(fp, gp);
+            continue;
+        }
+        int d = RMAX;
+        u32 h = ht_hash(id);
+        for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
+            const u32 cur = ht[h];
+            if (cur == id) { d = hidx[h]; break; }
+            if (cur == 0) break;
+        }
+        f64 cr, cg, cb, ca;
+        if (d < RMAX) {
+            record_colour<GOURAUD>(rec + d * St::REC, px, py, cr, cg, cb, ca);
+        } else {   // overflow: load this pixel's winner directly
+            f64 r[St::REC];
+            make_record<GOURAUD>(fp, (i64)id - 1, r);
+            record_colour<GOURAUD>(r, px, py, cr, cg, cb, ca);
+        }
+        store_pixel<ZMODE>(fp, gp, kv, cr, cg, cb, ca);
+    }
 }
 
 enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
@@ -355,11 +468,17 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
     // rows at the same column then hit different LDS banks
     __shared__ u64 key[TH * KS];
     __shared__ u32 zin[ZMODE == 2 ? TH * KS : 1];
-    __shared__ f64 S[NW][F_NSLOT][64];
-    __shared__ iu8 MAP[NW][64 * TH];
-    __shared__ iu8 RR0[NW][64];
-    __shared__ unsigned short ROFF[NW][64];
-    __shared__ u32 TT[NW][64];   // triangle id + 1 of each lane's triangle
+    // raster staging and shading staging share one LDS region
+    constexpr int O_MAP = NW * F_NSLOT * 64 * 8, O_RR0 = O_MAP + NW * 64 * TH, O_ROFF = O_RR0 + NW * 64,
+                  O_TT = O_ROFF + NW * 64 * 2, RASTER_BYTES = O_TT + NW * 64 * 4;
+    constexpr int SMEM = RASTER_BYTES > ShadeStage<GOURAUD>::BYTES ? RASTER_BYTES : ShadeStage<GOURAUD>::BYTES;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+    auto& S = *reinterpret_cast<f64 (*)[NW][F_NSLOT][64]>(smem);
+    auto& MAP = *reinterpret_cast<iu8 (*)[NW][64 * TH]>(smem + O_MAP);
+    auto& RR0 = *reinterpret_cast<iu8 (*)[NW][64]>(smem + O_RR0);
+    auto& ROFF = *reinterpret_cast<unsigned short (*)[NW][64]>(smem + O_ROFF);
+    auto& TT = *reinterpret_cast<u32 (*)[NW][64]>(smem + O_TT);   // triangle id + 1 of each lane's triangle
+    __shared__ u32 nU;
     __shared__ int sLast;
     __shared__ unsigned long long sFrag;
     if (!plan[3]) return;
@@ -384,7 +503,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         if (ls == le) {   // no triangle: only the pending clears
             for (int p = tid; p < TH * TW; p += VWG) {
                 const int lx = p & (TW - 1), ly = p / TW;
-                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, 0ull);
+                if (lx < wlim && ly < hlim) store_clear<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx);
             }
             continue;
         }
@@ -498,10 +617,8 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         }
         __syncthreads();
         if (!multi) {   // the whole list was in this slice: shade now
-            for (int p = tid; p < TH * TW; p += VWG) {
-                const int lx = p & (TW - 1), ly = p / TW;
-                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[ly * KS + lx]);
-            }
+            shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim,
+                                            [&](int p) { return key[(p / TW) * KS + (p & (TW - 1))]; }, smem, nU);
             continue;
         }
         // split tile: merge into the global keys; the last slice to finish
@@ -527,14 +644,16 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         }
         __syncthreads();
         if (!sLast) continue;
-        for (int p = tid; p < TH * TW; p += VWG) {
+        for (int p = tid; p < TH * TW; p += VWG) {   // merged keys -> LDS, global keys back to neutral
             const int lx = p & (TW - 1), ly = p / TW;
             if (lx >= wlim || ly >= hlim) continue;
             u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-            const u64 kv = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, kv);
+            key[ly * KS + lx] = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(g, ZMODE == 1 ? ~0ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        __syncthreads();
+        shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim,
+                                        [&](int p) { return key[(p / TW) * KS + (p & (TW - 1))]; }, smem, nU);
     }   // work items
     if (COUNT) {
         __syncthreads();

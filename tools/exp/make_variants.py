@@ -1,8 +1,8 @@
-"""Builds ablation variants of the order-free raster into tools/exp/<name>.so
-(A/B timing only; never shipped).  Each variant removes one stage of k_vis so
-the per-stage cost is the difference of two bench lines:
-  e0 full   e1 no shading (depth only)   e2 + no pixel loop   e3 + no row loop
-Other variants: name=DEF=VAL+DEF2=VAL (compile-time knobs, e.g. NR_VWG).
+"""Builds ablation / instrumentation variants of the order-free raster into
+tools/exp/<name>.so (A/B timing only; never shipped).  Named variants:
+  e1 no shading (depth only)   e2 + no pixel loop   e3 + no row loop
+  times  per-work-item start/end clocks (ExpGetItemTimes, tools/exp/item_times.py)
+Other variants: name=DEF=VAL+DEF2=VAL (compile-time knobs, e.g. NR_VWG, NR_SLICE).
 Usage: python tools/exp/make_variants.py [names...]; run with tools/exp/run.sh."""
 import os
 import subprocess
@@ -11,42 +11,79 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SRC = os.path.join(ROOT, "libnativecpurenderer_amd", "csrc")
 VARIANTS = {
-    "e0": [],
     "e1": ["EXP_NOSHADE"],
     "e2": ["EXP_NOSHADE", "EXP_NOPIX"],
     "e3": ["EXP_NOSHADE", "EXP_NOITEMS"],
+    "times": ["EXP_TIMES"],
 }
-PATCHES = [
-    ("            for (int it = lane; it < R; it += 64) {",
-     "            for (int it = lane; it < (EXP_NOITEMS ? 0 : R); it += 64) {"),
-    ("                if (COUNT) myFrags += (unsigned long long)(xe - xs);",
-     "                if (COUNT) myFrags += (unsigned long long)(xe - xs);\n"
-     "                if (EXP_NOPIX) { if (xe > 100) key[0] = xe; continue; }"),
-    ("                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[p]);",
-     "                if (EXP_NOSHADE) { if (lx < wlim && ly < hlim) fp.depth[(y0+ly)*fp.W+x0+lx] = (u32)key[p]; continue; }\n"
-     "                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[p]);"),
-]
+# define -> [(anchor, replacement)]; only the patches of the defines in use are applied
+PATCHES = {
+    "EXP_TIMES": [
+        ("    for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {\n",
+         "    u64 exp_t0 = 0; u32 exp_prev = ~0u; u64 exp_info = 0;\n"
+         "    for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {\n"
+         "        if (tid == 0) { const u64 now = __builtin_amdgcn_s_memrealtime();\n"
+         "            if (exp_prev != ~0u) exp_record(exp_prev, exp_t0, now, exp_info);\n"
+         "            exp_prev = item; exp_t0 = now; const uint4 dd = items[item];\n"
+         "            exp_info = (u64)(dd.z - dd.y) | ((u64)dd.w << 32) | ((u64)blockIdx.x << 48); }\n"),
+        ("    }   // work items\n",
+         "    }   // work items\n"
+         "    if (tid == 0 && exp_prev != ~0u) exp_record(exp_prev, exp_t0, __builtin_amdgcn_s_memrealtime(), exp_info);\n"),
+    ],
+    "EXP_NOITEMS": [
+        ("            for (int it = lane; it < R; it += 64) {",
+         "            for (int it = lane; it < (EXP_NOITEMS ? 0 : R); it += 64) {"),
+    ],
+    "EXP_NOPIX": [
+        ("                if (COUNT) myFrags += (unsigned long long)(xe - xs);",
+         "                if (COUNT) myFrags += (unsigned long long)(xe - xs);\n"
+         "                if (EXP_NOPIX) { if (xe > 100) key[0] = xe; continue; }"),
+    ],
+    "EXP_NOSHADE": [
+        ("                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[ly * KS + lx]);",
+         "                if (EXP_NOSHADE) { if (lx < wlim && ly < hlim) fp.depth[(y0+ly)*fp.W+x0+lx] = (u32)key[ly * KS + lx]; continue; }\n"
+         "                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[ly * KS + lx]);"),
+    ],
+}
+PRELUDE = """#include <hip/hip_runtime.h>
+__device__ unsigned long long g_exp[4 * 65536];
+__device__ inline void exp_record(unsigned item, unsigned long long t0, unsigned long long t1, unsigned long long info) {
+    if (item < 65536) { g_exp[4 * item] = t0; g_exp[4 * item + 1] = t1; g_exp[4 * item + 2] = info; }
+}
+"""
+HOST = """
+extern "C" int ExpGetItemTimes(unsigned long long* out, int n) {
+    if (n > 4 * 65536) n = 4 * 65536;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
+"""
+
+
+def parse(n):
+    if "=" in n:
+        n, spec = n.split("=", 1)
+        return n, [f"-D{d}" for d in spec.split("+")], []
+    return n, [f"-D{d}=1" for d in VARIANTS[n]], VARIANTS[n]
 
 
 def main(names):
+    specs = [parse(n) for n in names]
+    used = {d for _, _, ds in specs for d in ds}
     src = open(os.path.join(SRC, "nr_tri_free.hip")).read()
-    for a, b in PATCHES:
-        assert src.count(a) == 1, a
-        src = src.replace(a, b)
-    src = "#ifndef EXP_NOITEMS\n#define EXP_NOITEMS 0\n#endif\n#ifndef EXP_NOPIX\n#define EXP_NOPIX 0\n#endif\n" \
-          "#ifndef EXP_NOSHADE\n#define EXP_NOSHADE 0\n#endif\n" + src
+    for d in sorted(used):
+        for a, b in PATCHES[d]:
+            if src.count(a) != 1:
+                sys.exit(f"make_variants: anchor for {d} not found (update PATCHES):\n{a}")
+            src = src.replace(a, b)
+    defaults = "".join(f"#ifndef {d}\n#define {d} 0\n#endif\n" for d in PATCHES)
+    src = defaults + PRELUDE + src + HOST
     tmp = os.path.join(SRC, "_exp_tri_free.hip")
     open(tmp, "w").write(src)
     objs = [os.path.join(ROOT, "build", "obj", f) for f in sorted(os.listdir(os.path.join(ROOT, "build", "obj")))
             if f.endswith(".o") and f != "nr_tri_free.o"]
     procs = []
     try:
-        for n in names:
-            if "=" in n:
-                n, spec = n.split("=", 1)
-                defs = [f"-D{d}" for d in spec.split("+")]
-            else:
-                defs = [f"-D{d}=1" for d in VARIANTS[n]]
+        for n, defs, _ in specs:
             o = f"/tmp/_exp_{n}.o"
             cmd = (f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-gpu-rdc "
                    f"{' '.join(defs)} -I{SRC} -c {tmp} -o {o} && /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared "

@@ -3,7 +3,11 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 cp libnativecpurenderer_amd/libNativeCPURenderer.so /tmp/keep.so
 for v in "$@"; do
-  cp tools/exp/$v.so libnativecpurenderer_amd/libNativeCPURenderer.so
+  if [ "$v" = base ]; then cp /tmp/keep.so libnativecpurenderer_amd/libNativeCPURenderer.so; else cp tools/exp/$v.so libnativecpurenderer_amd/libNativeCPURenderer.so; fi
+  if [ "$v" = times ]; then
+    timeout -k 10 300 python tools/exp/item_times.py > gpurun_out/exp_$v.log 2>&1; rc=$?; cat gpurun_out/exp_$v.log | tail -12
+    [ $rc -eq 0 ] || break; continue
+  fi
   timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline $BENCH_ARGS > gpurun_out/exp_$v.log 2>&1
   rc=$?
   echo "$v rc=$rc $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/exp_$v.log) $(grep -o '"kernel_us": {[^}]*}' gpurun_out/exp_$v.log)"
