@@ -188,7 +188,9 @@ __device__ __forceinline__ f64 crossing_ceil(f64 b, f64 s, f64 c, bool& safe) {
 }
 
 // row_span_in with the per-edge slopes (no division unless a crossing lies
-// within eps of an integer, see crossing_ceil): the same [xs, xe).
+// within eps of an integer, see crossing_ceil): the same [xs, xe).  (k_vis
+// uses this form; row_span_in is its reference statement, and both are
+// checked against row_span in tests/test_oracle.py.)
 __device__ __forceinline__ void row_span_slopes(const f64 (&sx)[3], const f64 (&sy)[3], const f64 (&sl)[3], f64 y,
                                                 f64 x0, f64 wlim, int& xs, int& xe) {
     const bool b0 = sy[0] > y, b1 = sy[1] > y, b2 = sy[2] > y;

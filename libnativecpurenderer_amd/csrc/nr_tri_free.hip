@@ -16,10 +16,10 @@
 //   2 k_free_plan    one workgroup: exclusive scans of the tile counts (list
 //                    offsets) and of the slice counts (work items)
 //   3 k_free_emit    per-tile lists (order inside a list is irrelevant here)
-//   4 k_vis          one 256-thread workgroup per (tile, slice of <= 512
+//   4 k_vis          one 256-thread workgroup per (tile, slice of <= SLICE
 //                    triangles; an empty tile is one item): each wave takes
-//                    64-triangle chunks -> exact row spans -> depth + LDS
-//                    atomic on the tile's 2048 packed keys; then the same
+//                    64-triangle chunks, lane = triangle -> exact row spans ->
+//                    depth + LDS atomic on the tile's 2048 packed keys; then the same
 //                    workgroup shades the tile (deferred: winner ->
 //                    barycentrics -> colour -> ApplyPixel -> framebuffer,
 //                    depth and u8 frame written once).  A tile whose list is
@@ -440,24 +440,17 @@ __device__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int 
     }
 }
 
-enum { F_X0 = 0, F_Y0, F_X1, F_Y1, F_X2, F_Y2, F_INV, F_Z0, F_DZ1, F_DZ2, F_NSLOT };
 constexpr int NW = VWG / 64;   // waves per k_vis workgroup
 constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
-
-// Wave-synchronous ordering of this wave's own LDS traffic (a wave's LDS
-// operations complete in order; this stops the compiler from reordering them).
-__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
 
 // One workgroup per work item (tile, slice of <= SLICE triangles).  The 4
 // waves share only the tile's 2048 LDS keys; each wave independently walks
 // 64-triangle chunks of the slice (chunk c goes to wave c % 4) with no
-// workgroup barrier:
-//   setup   one lane per triangle: screen vertices, 1/den, depths, the rows of
-//           this tile it straddles (next chunk prefetched into registers)
-//   scan    exclusive scan of the row counts with wave shuffles, then each
-//           lane writes its triangle's lane index into a row->triangle map
-//   rows    the chunk's (triangle, row) items over the 64 lanes: exact span
-//           (row_span), then per pixel depth + LDS atomic on the packed key
+// workgroup barrier: one lane per triangle, its setup in registers (screen
+// vertices, edge slopes, 1/den, depths; the next chunk's loads in flight),
+// then the lane walks the triangle's rows in this tile (exact span,
+// row_span_slopes) and their pixels (depth + LDS atomic on the packed key,
+// two pixels per step).  Then the workgroup shades the tile (shade_tile).
 template <int ZMODE, bool COUNT, bool GOURAUD>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES_PER_EU))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
@@ -468,16 +461,8 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
     // rows at the same column then hit different LDS banks
     __shared__ u64 key[TH * KS];
     __shared__ u32 zin[ZMODE == 2 ? TH * KS : 1];
-    // raster staging and shading staging share one LDS region
-    constexpr int O_MAP = NW * F_NSLOT * 64 * 8, O_RR0 = O_MAP + NW * 64 * TH, O_ROFF = O_RR0 + NW * 64,
-                  O_TT = O_ROFF + NW * 64 * 2, RASTER_BYTES = O_TT + NW * 64 * 4;
-    constexpr int SMEM = RASTER_BYTES > ShadeStage<GOURAUD>::BYTES ? RASTER_BYTES : ShadeStage<GOURAUD>::BYTES;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
-    auto& S = *reinterpret_cast<f64 (*)[NW][F_NSLOT][64]>(smem);
-    auto& MAP = *reinterpret_cast<iu8 (*)[NW][64 * TH]>(smem + O_MAP);
-    auto& RR0 = *reinterpret_cast<iu8 (*)[NW][64]>(smem + O_RR0);
-    auto& ROFF = *reinterpret_cast<unsigned short (*)[NW][64]>(smem + O_ROFF);
-    auto& TT = *reinterpret_cast<u32 (*)[NW][64]>(smem + O_TT);   // triangle id + 1 of each lane's triangle
+    // shading staging (ShadeStage)
+    __shared__ __attribute__((aligned(16))) unsigned char smem[ShadeStage<GOURAUD>::BYTES];
     __shared__ u32 nU;
     __shared__ int sLast;
     __shared__ unsigned long long sFrag;
@@ -518,7 +503,9 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         }
         __syncthreads();
 
-        // this wave's chunks: c = wave, wave + NW, ...
+        // this wave's chunks: c = wave, wave + NW, ...  One lane per triangle,
+        // its setup in registers; the lane walks the triangle's rows in this
+        // tile (exact span from the per-edge slopes) and their pixels.
         const u32 nch = (le - ls + 63) / 64;
         u32 pt = 0;
         f64 pxy[6], pz[3] = {0, 0, 0};
@@ -537,72 +524,38 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         for (u32 c = wave; c < nch; c += NW) {
             const u32 base = ls + c * 64;
             const int cnt = (le - base) < 64u ? (int)(le - base) : 64;
-            // ---- setup (lane = triangle)
             const u32 t = pt;
-            int r0 = 0, nr = 0;
-            if (lane < cnt) {
-                f64 sx[3], sy[3];
+            f64 sx[3], sy[3], sl[3];
 #pragma unroll
-                for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
-                const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-                const f64 den = e1x * e2y - e2x * e1y;
-                const bool ok = tri_finite(sx, sy) && den != 0;
-                S[wave][F_X0][lane] = sx[0]; S[wave][F_Y0][lane] = sy[0];
-                S[wave][F_X1][lane] = sx[1]; S[wave][F_Y1][lane] = sy[1];
-                S[wave][F_X2][lane] = sx[2]; S[wave][F_Y2][lane] = sy[2];
-                S[wave][F_INV][lane] = 1.0 / den;
-                if (DEPTH) {
-                    S[wave][F_Z0][lane] = pz[0]; S[wave][F_DZ1][lane] = pz[1] - pz[0];
-                    S[wave][F_DZ2][lane] = pz[2] - pz[0];
-                }
-                if (ok) {
-                    // rows with a straddling edge: ymin <= y < ymax (exact)
-                    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
-                    r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
-                    const int r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
-                    nr = r1 > r0 ? r1 - r0 : 0;
-                }
-            }
+            for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
+            const f64 zz0 = pz[0], dz1 = pz[1] - pz[0], dz2 = pz[2] - pz[0];
             prefetch(c + NW);
-            // ---- scan of the row counts, row -> triangle map
-            int incl = nr;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int o = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += o;
+            const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+            const f64 den = e1x * e2y - e2x * e1y;
+            int r0 = 0, r1 = 0;   // rows with a straddling edge: ymin <= y < ymax (exact)
+            if (lane < cnt && tri_finite(sx, sy) && den != 0) {
+                const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+                r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
+                r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
             }
-            const int ex = incl - nr;
-            const int R = __shfl(incl, 63, 64);
-            TT[wave][lane] = t + 1;
-            RR0[wave][lane] = (iu8)r0;
-            ROFF[wave][lane] = (unsigned short)ex;
-            for (int j = 0; j < nr; ++j) MAP[wave][ex + j] = (iu8)lane;
-            wave_lds_fence();
-            // ---- (triangle, row) items over the lanes
+            if (r0 >= r1) continue;
+            edge_slopes(sx, sy, sl);
+            const f64 inv = 1.0 / den;
+            const u64 id1 = (u64)t + 1;
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-            for (int it = lane; it < R; it += 64) {
-                const int k = MAP[wave][it];
-                const int r = RR0[wave][k] + (it - ROFF[wave][k]);
-                const f64 sx[3] = {S[wave][F_X0][k], S[wave][F_X1][k], S[wave][F_X2][k]};
-                const f64 sy[3] = {S[wave][F_Y0][k], S[wave][F_Y1][k], S[wave][F_Y2][k]};
+            for (int r = r0; r < r1; ++r) {
                 const f64 y = (f64)(int)(y0 + r);
                 int xs, xe;
-                row_span_in(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);
+                row_span_slopes(sx, sy, sl, y, (f64)x0, (f64)wlim, xs, xe);
                 if (COUNT) myFrags += (unsigned long long)(xe - xs);
                 if (xs >= xe) continue;
-                const u64 id1 = TT[wave][k];
                 if (ZMODE == 0) {
 #pragma clang loop vectorize(disable) interleave(disable)
                     for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * KS + lx], id1);
                     continue;
                 }
-                const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-                const f64 inv = S[wave][F_INV][k];
-                const f64 zz0 = S[wave][F_Z0][k], dz1 = S[wave][F_DZ1][k], dz2 = S[wave][F_DZ2][k];
                 const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
-                f64 X = (f64)(int)(x0 + xs);   // pixel x as f64, exact (integers < 2^31)
-#pragma clang loop vectorize(disable) interleave(disable)
-                for (int lx = xs; lx < xe; ++lx, X += 1.0) {
+                auto frag = [&](int lx, f64 X) {
                     const f64 dx = X - sx[0];
                     const f64 w1 = (dx * e2y - e2x * dy) * inv;
                     const f64 w2 = (e1x * dy - dx * e1y) * inv;
@@ -611,9 +564,16 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
                     const int p = r * KS + lx;
                     if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
                     else if (zq < zin[p]) atomicMax(&key[p], id1);
+                };
+                // two pixels per step: independent chains (ILP) and half the
+                // divergent trip count for the short spans of sliver triangles
+                f64 X = (f64)(int)(x0 + xs);   // pixel x as f64, exact (integers < 2^31)
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+                for (int lx = xs; lx < xe; lx += 2, X += 2.0) {
+                    frag(lx, X);
+                    if (lx + 1 < xe) frag(lx + 1, X + 1.0);
                 }
             }
-            wave_lds_fence();   // the next chunk overwrites this wave's staging
         }
         __syncthreads();
         if (!multi) {   // the whole list was in this slice: shade now

@@ -191,6 +191,34 @@ def py_row_span_in(y, pts):
     return math.ceil(min(c)), math.ceil(max(c))
 
 
+def py_row_span_slopes(y, pts):
+    """nr_tri.h row_span_slopes: per-edge slopes, a division only when a
+    crossing lies within eps of an integer (crossing_ceil)."""
+    sx = [p[0] for p in pts]
+    sy = [p[1] for p in pts]
+
+    def slope(i, j):
+        d = sy[j] - sy[i]
+        return (sx[j] - sx[i]) / d if d != 0 else math.inf
+    sl = [slope(0, 2), slope(1, 0), slope(2, 1)]
+    b = [v > y for v in sy]
+    v1 = b[1] != b[0] and b[1] != b[2]
+    v2 = b[2] != b[0] and b[2] != b[1]
+    ea, sa = ((2, 1), sl[2]) if v1 else ((0, 2), sl[0])
+    eb, sb = ((2, 1), sl[2]) if v2 else ((1, 0), sl[1])
+    ks, safe = [], True
+    for (i, _), s_ in ((ea, sa), (eb, sb)):
+        v = (y - sy[i]) * s_
+        cc = v + sx[i]
+        k = math.ceil(cc) if math.isfinite(cc) else 0
+        eps = (abs(v) + abs(cc)) * 2.0 ** -50 + 2.0 ** -1000
+        safe = safe and (cc - (k - 1.0) > eps) and (k - cc > eps)
+        ks.append(k)
+    if not safe:
+        ks = [math.ceil((sx[j] - sx[i]) * (y - sy[i]) / (sy[j] - sy[i]) + sx[i]) for i, j in (ea, eb)]
+    return min(ks), max(ks), safe
+
+
 def _edge_case_triangles():
     g = scenes.rng(77)
     tris = [
@@ -219,6 +247,31 @@ def test_branchless_row_span_equals_row_span():
         ys = [p[1] for p in pts]
         for y in range(math.ceil(min(ys)), math.ceil(max(ys))):
             assert py_row_span_in(float(y), pts) == py_row_span(float(y), pts), (pts, y)
+
+
+def test_slope_row_span_equals_row_span():
+    g = scenes.rng(5)
+    tris = list(_edge_case_triangles())
+    for _ in range(3000):   # arbitrary geometry: the fast path is taken and must agree
+        c = g.uniform(-50, 4000, 2)
+        tris.append([tuple(c + g.normal(0, 6, 2)) for _ in range(3)])
+    for _ in range(1000):   # integer / half-integer vertices: crossings land on integers
+        c = g.integers(0, 60, 2)
+        tris.append([tuple((c + g.integers(-8, 9, 2)) / g.choice([1, 2, 4])) for _ in range(3)])
+    for _ in range(300):    # huge coordinates
+        c = g.uniform(-1e9, 1e9, 2)
+        tris.append([tuple(c + g.normal(0, 1e6, 2)) for _ in range(3)])
+    fast = 0
+    total = 0
+    for pts in tris:
+        ys = [p[1] for p in pts]
+        lo, hi = math.ceil(min(ys)), math.ceil(max(ys))
+        for y in range(lo, min(hi, lo + 40)):
+            a, b, safe = py_row_span_slopes(float(y), pts)
+            assert (a, b) == py_row_span(float(y), pts), (pts, y)
+            fast += safe
+            total += 1
+    assert fast > total // 2
 
 
 def test_oracle_triangle_coverage_equals_point_in_polygon(oracle):

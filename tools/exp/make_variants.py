@@ -1,6 +1,6 @@
 """Builds ablation / instrumentation variants of the order-free raster into
 tools/exp/<name>.so (A/B timing only; never shipped).  Named variants:
-  e1 no shading (depth only)   e2 + no pixel loop   e3 + no row loop
+  e1 no shading of single-slice tiles   e2 + no pixel loop   e3 + no row loop   e4 + no raster
   times  per-work-item start/end clocks (ExpGetItemTimes, tools/exp/item_times.py)
 Other variants: name=DEF=VAL+DEF2=VAL (compile-time knobs, e.g. NR_VWG, NR_SLICE).
 Usage: python tools/exp/make_variants.py [names...]; run with tools/exp/run.sh."""
@@ -13,7 +13,9 @@ SRC = os.path.join(ROOT, "libnativecpurenderer_amd", "csrc")
 VARIANTS = {
     "e1": ["EXP_NOSHADE"],
     "e2": ["EXP_NOSHADE", "EXP_NOPIX"],
-    "e3": ["EXP_NOSHADE", "EXP_NOITEMS"],
+    "e3": ["EXP_NOSHADE", "EXP_NOROWS"],
+    "e4": ["EXP_NOSHADE", "EXP_NORASTER"],
+    "na": ["EXP_NOATOMIC"],
     "times": ["EXP_TIMES"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
@@ -30,19 +32,27 @@ PATCHES = {
          "    }   // work items\n"
          "    if (tid == 0 && exp_prev != ~0u) exp_record(exp_prev, exp_t0, __builtin_amdgcn_s_memrealtime(), exp_info);\n"),
     ],
-    "EXP_NOITEMS": [
-        ("            for (int it = lane; it < R; it += 64) {",
-         "            for (int it = lane; it < (EXP_NOITEMS ? 0 : R); it += 64) {"),
+    "EXP_NOROWS": [
+        ("            if (r0 >= r1) continue;\n",
+         "            if (r0 >= r1) continue;\n            if (EXP_NOROWS) { if (r1 > 1000) key[0] = r0; continue; }\n"),
     ],
     "EXP_NOPIX": [
-        ("                if (COUNT) myFrags += (unsigned long long)(xe - xs);",
-         "                if (COUNT) myFrags += (unsigned long long)(xe - xs);\n"
-         "                if (EXP_NOPIX) { if (xe > 100) key[0] = xe; continue; }"),
+        ("                if (xs >= xe) continue;\n                if (ZMODE == 0) {",
+         "                if (xs >= xe) continue;\n                if (EXP_NOPIX) { if (xe > 100) key[0] = xe; continue; }\n"
+         "                if (ZMODE == 0) {"),
     ],
     "EXP_NOSHADE": [
-        ("                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[ly * KS + lx]);",
-         "                if (EXP_NOSHADE) { if (lx < wlim && ly < hlim) fp.depth[(y0+ly)*fp.W+x0+lx] = (u32)key[ly * KS + lx]; continue; }\n"
-         "                if (lx < wlim && ly < hlim) resolve_pixel<ZMODE, GOURAUD>(fp, x0 + lx, y0 + ly, key[ly * KS + lx]);"),
+        ("        if (!multi) {   // the whole list was in this slice: shade now\n",
+         "        if (EXP_NOSHADE && !multi) continue;\n        if (!multi) {   // the whole list was in this slice: shade now\n"),
+    ],
+    "EXP_NOATOMIC": [
+        ("                    if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);",
+         "                    if (ZMODE == 1 && EXP_NOATOMIC) key[p] = ((u64)zq << 32) | id1;\n"
+         "                    else if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);"),
+    ],
+    "EXP_NORASTER": [
+        ("        for (u32 c = wave; c < nch; c += NW) {",
+         "        for (u32 c = wave; c < (EXP_NORASTER ? 0u : nch); c += NW) {"),
     ],
 }
 PRELUDE = """#include <hip/hip_runtime.h>
