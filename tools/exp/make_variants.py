@@ -16,6 +16,9 @@ VARIANTS = {
     "e3": ["EXP_NOSHADE", "EXP_NOROWS"],
     "e4": ["EXP_NOSHADE", "EXP_NORASTER"],
     "na": ["EXP_NOATOMIC"],
+    "nf64": ["EXP_NOF64ST"],
+    "nu8": ["EXP_NOU8ST"],
+    "nst": ["EXP_NOF64ST", "EXP_NOU8ST"],
     "times": ["EXP_TIMES"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
@@ -49,6 +52,18 @@ PATCHES = {
         ("                    if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);",
          "                    if (ZMODE == 1 && EXP_NOATOMIC) key[p] = ((u64)zq << 32) | id1;\n"
          "                    else if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);"),
+    ],
+    "EXP_NOF64ST": [   # shading skips the f64 framebuffer stores (u8 frame and depth still written)
+        ("    dst[0] = cr; dst[1] = cg; dst[2] = cb;\n    if (ipp == 4) dst[3] = ca;\n",
+         "    if (!EXP_NOF64ST) { dst[0] = cr; dst[1] = cg; dst[2] = cb;\n    if (ipp == 4) dst[3] = ca; }\n"),
+        ("        dst[0] = v; dst[1] = v; dst[2] = v;\n        if (ipp == 4) dst[3] = v;\n",
+         "        if (!EXP_NOF64ST) { dst[0] = v; dst[1] = v; dst[2] = v;\n        if (ipp == 4) dst[3] = v; }\n"),
+    ],
+    "EXP_NOU8ST": [   # shading skips the u8 frame stores
+        ("    if (fp.frameU8) {\n        iu8* d8 = fp.frameU8 + p * ipp;\n        d8[0] = nr_to_u8(cr);",
+         "    if (fp.frameU8 && !EXP_NOU8ST) {\n        iu8* d8 = fp.frameU8 + p * ipp;\n        d8[0] = nr_to_u8(cr);"),
+        ("        if (fp.frameU8) {\n            iu8* d8 = fp.frameU8 + p * ipp;",
+         "        if (fp.frameU8 && !EXP_NOU8ST) {\n            iu8* d8 = fp.frameU8 + p * ipp;"),
     ],
     "EXP_NORASTER": [
         ("        for (u32 c = wave; c < nch; c += NW) {",
