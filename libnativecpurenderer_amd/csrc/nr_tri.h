@@ -38,7 +38,11 @@ struct BinParams {
     int nshards, shard;   // owned tile rows: ty % nshards == shard
 };
 
-__device__ __forceinline__ bool owned_row(int ty, int nshards, int shard) { return ty % nshards == shard; }
+// (unsharded: no integer division -- it costs ~30 VALU instructions)
+__device__ __forceinline__ bool owned_row(int ty, int nshards, int shard) { return nshards == 1 || ty % nshards == shard; }
+__device__ __forceinline__ bool owned_tile(int tile, int tiles_x, int nshards, int shard) {
+    return nshards == 1 || (tile / tiles_x) % nshards == shard;
+}
 
 __device__ __forceinline__ f64 clampd(f64 v, f64 lo, f64 hi) { return v < lo ? lo : (v > hi ? hi : v); }
 

@@ -19,6 +19,7 @@ VARIANTS = {
     "nf64": ["EXP_NOF64ST"],
     "nu8": ["EXP_NOU8ST"],
     "nst": ["EXP_NOF64ST", "EXP_NOU8ST"],
+    "plant": ["EXP_PLANT"],
     "times": ["EXP_TIMES"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
@@ -64,6 +65,18 @@ PATCHES = {
          "    if (fp.frameU8 && !EXP_NOU8ST) {\n        iu8* d8 = fp.frameU8 + p * ipp;\n        d8[0] = nr_to_u8(cr);"),
         ("        if (fp.frameU8) {\n            iu8* d8 = fp.frameU8 + p * ipp;",
          "        if (fp.frameU8 && !EXP_NOU8ST) {\n            iu8* d8 = fp.frameU8 + p * ipp;"),
+    ],
+    "EXP_PLANT": [   # s_memrealtime stamps at the plan kernel's phase boundaries -> g_exp[0..5]
+        ("    if (tid < PLAN_NB) bcnt[tid] = 0;\n    __syncthreads();\n    // pass 1",
+         "    const u64 pt0 = __builtin_amdgcn_s_memrealtime();\n    if (tid < PLAN_NB) bcnt[tid] = 0;\n    __syncthreads();\n    // pass 1"),
+        ("    __syncthreads();\n    // pass 2: offsets and items\n",
+         "    __syncthreads();\n    const u64 pt1 = __builtin_amdgcn_s_memrealtime();\n    // pass 2: offsets and items\n"),
+        ("        off[ntiles] = ta;\n",
+         "        off[ntiles] = ta;\n        const u64 pt2 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);\n    }\n}",
+         "        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+         "        const u64 pt3 = __builtin_amdgcn_s_memrealtime();\n"
+         "        g_exp[0] = pt0; g_exp[1] = pt1; g_exp[2] = pt2; g_exp[3] = pt3; g_exp[4] = ntiles;\n    }\n}"),
     ],
     "EXP_NORASTER": [
         ("        for (u32 c = wave; c < nch; c += NW) {",
