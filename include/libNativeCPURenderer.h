@@ -117,6 +117,21 @@ void GetFrameU8(RenderContext* ctx, iu8* out);
 void* GetFrameU8DevicePtr(RenderContext* ctx);
 bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root); /* f64 + depth bands to root */
 
+/* ---- NEW: deferred command list ---------------------------
+ * Replaces the reference's recording proxy MultiThreadedVideoRenderContext-
+ * Preparer (libNativeCPURendererPybind.py:302-367, whose replay is a stub).
+ * While recording, DrawTexture / DrawSplittedTexture / DrawRect / DrawLine /
+ * DrawCircle / DrawVerticalGrd / FillColor / ApplyPixel / SetPixel are queued
+ * and then run together by ONE launch, per pixel in recording order, with the
+ * exact results of the immediate calls (every pixel read and written once per
+ * list instead of once per draw).  Any call that reads or otherwise touches
+ * the framebuffer runs the queue first; SetColor discards it (overwritten). */
+void BeginCommandList(RenderContext* ctx);       /* start queueing primitive draws */
+void EndCommandList(RenderContext* ctx);         /* run the queue, stop queueing */
+void FlushCommandList(RenderContext* ctx);       /* run the queue, keep queueing (end of a frame) */
+i64 GetCommandListLength(RenderContext* ctx);    /* draws queued and not yet run */
+bool IsRecordingCommands(RenderContext* ctx);
+
 /* ---- NEW: device, sync, interop, errors, measurement --------------------- */
 bool SetDevice(i64 device);                      /* device for objects created next on this thread */
 i64 GetDeviceCount(void);

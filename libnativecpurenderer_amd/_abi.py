@@ -102,6 +102,11 @@ DEVICE_ABI = {
     "GetKernelTiming": (B, (P, ctypes.c_char_p, P, P)),
     "ResetKernelTiming": (None, (P,)),
     "SetKernelTimingFilter": (None, (P, ctypes.c_char_p)),
+    "BeginCommandList": (None, (P,)),
+    "EndCommandList": (None, (P,)),
+    "FlushCommandList": (None, (P,)),
+    "GetCommandListLength": (L, (P,)),
+    "IsRecordingCommands": (B, (P,)),
 }
 
 HIP_LIBRARY_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **DEVICE_ABI}

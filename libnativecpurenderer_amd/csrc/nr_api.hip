@@ -74,11 +74,14 @@ void nr_settle_all() {
         std::lock_guard<std::mutex> lk(g_ctx_mu);
         v = g_ctxs;
     }
+    int prev = 0;
+    NR_CHECK(hipGetDevice(&prev));
     for (RenderContext* c : v)
-        if (c->pendingBatch) {
+        if (c->pendingBatch || c->cmdList) {
             NR_CHECK(hipSetDevice(c->device));
             nr_settle(c);
         }
+    NR_CHECK(hipSetDevice(prev));
 }
 
 static int current_device() {
@@ -313,6 +316,7 @@ RenderContext* CreateRenderContext(i64 width, i64 height, bool enableAlpha) {
 void DestroyRenderContext(RenderContext* ctx) {
     if (!ctx) return;
     NR_CHECK(hipSetDevice(ctx->device));
+    nr_free_commands(ctx);   // queued draws of a destroyed context are dead
     nr_settle(ctx);
     {
         std::lock_guard<std::mutex> lk(g_ctx_mu);
@@ -456,6 +460,7 @@ Texture* CreateTextureUInt8(i64 width, i64 height, bool enableAlpha, iu8* buffer
 // cpp:356-360 (no-op in the reference); aliases never free the framebuffer
 void DestroyTexture(Texture* t) {
     if (!t) return;
+    nr_settle_all();   // recorded draws that sample this texture run first
     if (t->owns && t->buffer) {
         NR_CHECK(hipSetDevice(t->device));
         NR_CHECK(hipStreamSynchronize(nr_stream_for(t->device)));
@@ -536,7 +541,12 @@ void ApplyTransform(RenderContext* ctx, f64 a, f64 b, f64 c, f64 d, f64 e, f64 f
 void Scale(RenderContext* ctx, f64 sx, f64 sy) { ApplyTransform(ctx, sx, 0, 0, sy, 0, 0); }    // cpp:420-426
 void Translate(RenderContext* ctx, f64 tx, f64 ty) { ApplyTransform(ctx, 1, 0, 0, 1, tx, ty); } // cpp:428-434
 void Rotate(RenderContext* ctx, f64 angle) {                                                   // cpp:436-444
-    f64 s = sin(angle), c = cos(angle);
+    // The reference is built with g++ -O3 (src/compile.sh), which merges the
+    // sin/cos pair of cpp:440-441 into one glibc sincos() call; sincos differs
+    // from separate sin and cos in the last bit for some angles (found by
+    // tests/test_command_list.py's random mixes), so call it explicitly.
+    f64 s, c;
+    sincos(angle, &s, &c);
     ApplyTransform(ctx, c, s, -s, c, 0, 0);
 }
 
@@ -575,6 +585,7 @@ void ApplyColorTransform(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
 bool SetPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
     if (x < 0 || x >= ctx->width || y < 0 || y >= ctx->height) return false;
     ctx->frameU8Valid = false;
+    if (ctx->recording) return nr_record_set_pixel(ctx, x, y, r, g, b, a);
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
     i64 ipp = ctx->enableAlpha ? 4 : 3;
@@ -593,6 +604,7 @@ __global__ void k_apply_one(f64* p, int ipp, f64 r, f64 g, f64 b, f64 a, f64 c0,
 bool ApplyPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
     if (x < 0 || x >= ctx->width || y < 0 || y >= ctx->height) return false;
     ctx->frameU8Valid = false;
+    if (ctx->recording) return nr_record_fill(ctx, x, x + 1, y, y + 1, r, g, b, a);
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
     int ipp = ctx->enableAlpha ? 4 : 3;
@@ -606,6 +618,7 @@ bool ApplyPixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
 void SetColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
     ctx->frameU8Valid = false;
     NR_CHECK(hipSetDevice(ctx->device));
+    nr_drop_commands(ctx);   // every value of the buffer is overwritten: queued draws are dead
     nr_settle(ctx);
     if (r == g && g == b && b == a) {
         // uniform clear: kept pending, consumed on chip by the tiled raster
@@ -644,6 +657,10 @@ void GetColor(RenderContext* ctx, f64 x, f64 y, f64* r, f64* g, f64* b, f64* a) 
 // cpp:682-691
 void FillColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
     ctx->frameU8Valid = false;
+    if (ctx->recording) {
+        nr_record_fill(ctx, 0, ctx->width, 0, ctx->height, r, g, b, a);
+        return;
+    }
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
     i64 n = ctx->width * ctx->height;

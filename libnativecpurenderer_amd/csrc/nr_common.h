@@ -100,6 +100,11 @@ struct RenderContext {
     bool frameOutput = false;   // set by GatherFrameU8: resolves also write the u8 frame
     bool frameU8Valid = false;  // frameU8 holds the u8 image of every owned pixel
     void* pendingBatch = nullptr;   // last visibility batch awaiting validation (nr_settle)
+    // deferred command list (BeginCommandList / EndCommandList, nr_prims.hip):
+    // while recording, primitive draws are queued and run together, in
+    // order, by one launch (every pixel read and written once)
+    bool recording = false;
+    void* cmdList = nullptr;
 };
 
 struct Texture {
@@ -131,8 +136,13 @@ void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
 void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);
 void nr_fill_f64(hipStream_t s, f64* p, i64 n, f64 v);
 void nr_fill_u32(hipStream_t s, u32* p, i64 n, u32 v);
-void nr_settle(RenderContext* ctx);               // validate an asynchronously sized batch
+void nr_settle(RenderContext* ctx);               // validate an asynchronously sized batch, run queued commands
 void nr_settle_all();                             // ... of every live context
+void nr_flush_commands(RenderContext* ctx);       // run the recorded primitive draws (nr_prims.hip)
+void nr_drop_commands(RenderContext* ctx);        // discard them (the whole buffer is overwritten next)
+void nr_free_commands(RenderContext* ctx);        // discard and release the list storage
+bool nr_record_fill(RenderContext* ctx, i64 i0, i64 i1, i64 j0, i64 j1, f64 r, f64 g, f64 b, f64 a);  // ApplyPixel over a range
+bool nr_record_set_pixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a);
 
 // x86-64 cvttsd2si semantics for (i64)double: out of range / NaN -> INT64_MIN
 static inline i64 nr_f2i64(f64 v) {

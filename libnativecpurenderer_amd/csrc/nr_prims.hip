@@ -15,10 +15,11 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 namespace {
 
-enum PrimMode { PM_RECT = 0, PM_TEX, PM_SPLIT, PM_VGRD, PM_CIRCLE, PM_LINE, PM_TEX_FAST };
+enum PrimMode { PM_RECT = 0, PM_TEX, PM_SPLIT, PM_VGRD, PM_CIRCLE, PM_LINE, PM_TEX_FAST, PM_FILL, PM_SETPIX };
 
 struct PrimParams {
     f64* buf;
@@ -39,14 +40,12 @@ struct PrimParams {
     f64 pts[4][2];           // DrawLine polygon (user space)
 };
 
+// Colour of pixel (i, j) under draw p; false when the draw does not cover it.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_prim(const PrimParams p) {
-    const i64 li = (i64)blockIdx.x * 64 + threadIdx.x;
-    const i64 lj = (i64)blockIdx.y * 4 + threadIdx.y;
-    if (li >= p.ni || lj >= p.nj) return;
-    const i64 i = p.i0 + li, j = p.j0 + lj;
-    f64 r, g, b, a;
-    if constexpr (MODE == PM_TEX_FAST) {
+__device__ __forceinline__ bool prim_pixel(const PrimParams& p, i64 i, i64 j, f64& r, f64& g, f64& b, f64& a) {
+    if constexpr (MODE == PM_FILL) {
+        r = p.c[0]; g = p.c[1]; b = p.c[2]; a = p.c[3];
+    } else if constexpr (MODE == PM_TEX_FAST) {
         // cpp:741-750 (IsNoTransform path; the transform is ignored)
         f64 u = ((f64)i - p.x) * p.sx;
         f64 v = ((f64)j - p.y) * p.sy;
@@ -58,18 +57,18 @@ __global__ __launch_bounds__(256) void k_prim(const PrimParams p) {
             // cpp:937-946
             f64 dx = ix - p.x, dy = iy - p.y;
             f64 dist = sqrt(dx * dx + dy * dy);
-            if (dist > p.radius) return;
+            if (dist > p.radius) return false;
             r = p.c[0]; g = p.c[1]; b = p.c[2]; a = p.c[3];
         } else if constexpr (MODE == PM_LINE) {
             // cpp:908-917
-            if (!nr_point_in_polygon<4>(ix, iy, p.pts)) return;
+            if (!nr_point_in_polygon<4>(ix, iy, p.pts)) return false;
             r = p.c[0]; g = p.c[1]; b = p.c[2]; a = p.c[3];
         } else {
             // inclusive quad test, cpp:866-869 / 764-767 / 806-809 / 1302-1305
-            if (ix < p.x) return;
-            if (ix > p.x + p.w) return;
-            if (iy < p.y) return;
-            if (iy > p.y + p.h) return;
+            if (ix < p.x) return false;
+            if (ix > p.x + p.w) return false;
+            if (iy < p.y) return false;
+            if (iy > p.y + p.h) return false;
             if constexpr (MODE == PM_RECT) {
                 r = p.c[0]; g = p.c[1]; b = p.c[2]; a = p.c[3];
             } else if constexpr (MODE == PM_VGRD) {
@@ -91,8 +90,125 @@ __global__ __launch_bounds__(256) void k_prim(const PrimParams p) {
             }
         }
     }
+    return true;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_prim(const PrimParams p) {
+    const i64 li = (i64)blockIdx.x * 64 + threadIdx.x;
+    const i64 lj = (i64)blockIdx.y * 4 + threadIdx.y;
+    if (li >= p.ni || lj >= p.nj) return;
+    const i64 i = p.i0 + li, j = p.j0 + lj;
+    f64 r, g, b, a;
+    if (!prim_pixel<MODE>(p, i, j, r, g, b, a)) return;
     nr_apply_pixel(p.buf + (j * p.W + i) * p.ipp, p.ipp, r, g, b, a, p.ct[0], p.ct[1], p.ct[2], p.ct[3]);
 }
+
+// ---- deferred command list ----------------------------------------------
+// Recorded draws (the same PrimParams the immediate launches take, bounds
+// included) run in one launch: a workgroup owns a CL_W x CL_H screen tile,
+// each thread CL_R pixels of one column, held in registers from the first
+// command to the last.  Commands are applied in recording order per pixel,
+// with the same per-pixel arithmetic (prim_pixel + ApplyPixel), so the result
+// equals the immediate sequence bit for bit, while the framebuffer is read and
+// written once per list instead of once per draw.  A tile skips a command
+// whose pixel range misses it (wave-uniform test on scalar loads).
+struct NrCmd {
+    int mode;
+    PrimParams p;
+};
+constexpr int CL_W = 64, CL_H = 16, CL_R = CL_H / 4;
+
+// ApplyPixel (cpp:515-549) on a register-resident pixel (nr_apply_pixel's
+// expressions).
+__device__ __forceinline__ void apply_reg(f64 (&px)[4], int ipp, f64 r, f64 g, f64 b, f64 a, const f64* ct) {
+    r *= ct[0]; g *= ct[1]; b *= ct[2]; a *= ct[3];
+    if (a != 1) {
+        r = px[0] * (1 - a) + r * a;
+        g = px[1] * (1 - a) + g * a;
+        b = px[2] * (1 - a) + b * a;
+    }
+    px[0] = r; px[1] = g; px[2] = b;
+    if (ipp == 4) px[3] = a;
+}
+
+template <int MODE>
+__device__ __forceinline__ void cmd_apply(const PrimParams& p, i64 i, i64 j0, int ipp, f64 (&px)[CL_R][4],
+                                          bool (&dirty)[CL_R], i64 W, i64 H) {
+    const bool colIn = i >= p.i0 && i < p.i0 + p.ni;
+#pragma unroll
+    for (int r = 0; r < CL_R; ++r) {
+        const i64 j = j0 + 4 * r;
+        if (!colIn || j < p.j0 || j >= p.j0 + p.nj) continue;
+        if constexpr (MODE == PM_SETPIX) {
+            // SetPixel (cpp:494-513): raw store of the target pixel; for RGB the
+            // reference also writes index+3 = channel 0 of the next pixel (A.6)
+            if (i == (i64)p.x && j == (i64)p.y) {
+                px[r][0] = p.c[0]; px[r][1] = p.c[1]; px[r][2] = p.c[2];
+                if (ipp == 4) px[r][3] = p.c[3];
+                dirty[r] = true;
+            } else if (ipp == 3 && i == (i64)p.sx && j == (i64)p.sy) {
+                px[r][0] = p.c[3];
+                dirty[r] = true;
+            }
+        } else {
+            f64 cr, cg, cb, ca;
+            if (!prim_pixel<MODE>(p, i, j, cr, cg, cb, ca)) continue;
+            apply_reg(px[r], ipp, cr, cg, cb, ca, p.ct);
+            dirty[r] = true;
+        }
+    }
+}
+
+template <int IPP>
+__global__ __launch_bounds__(256) void k_cmd_list(const NrCmd* __restrict__ cmds, int ncmd, f64* __restrict__ buf,
+                                                  i64 W, i64 H, int pend, f64 pendValue) {
+    const i64 tx0 = (i64)blockIdx.x * CL_W, ty0 = (i64)blockIdx.y * CL_H;
+    const i64 i = tx0 + threadIdx.x;
+    const i64 j0 = ty0 + threadIdx.y;
+    f64 px[CL_R][4];
+    bool dirty[CL_R];
+#pragma unroll
+    for (int r = 0; r < CL_R; ++r) {
+        const i64 j = j0 + 4 * r;
+        dirty[r] = pend != 0;
+        px[r][0] = px[r][1] = px[r][2] = px[r][3] = pendValue;
+        if (!pend && i < W && j < H) {
+            const f64* q = buf + (j * W + i) * IPP;
+            px[r][0] = q[0]; px[r][1] = q[1]; px[r][2] = q[2];
+            if (IPP == 4) px[r][3] = q[3];
+        }
+    }
+    for (int c = 0; c < ncmd; ++c) {
+        const PrimParams& p = cmds[c].p;
+        if (p.i0 >= tx0 + CL_W || p.i0 + p.ni <= tx0 || p.j0 >= ty0 + CL_H || p.j0 + p.nj <= ty0) continue;
+        switch (cmds[c].mode) {
+            case PM_RECT: cmd_apply<PM_RECT>(p, i, j0, IPP, px, dirty, W, H); break;
+            case PM_TEX: cmd_apply<PM_TEX>(p, i, j0, IPP, px, dirty, W, H); break;
+            case PM_SPLIT: cmd_apply<PM_SPLIT>(p, i, j0, IPP, px, dirty, W, H); break;
+            case PM_VGRD: cmd_apply<PM_VGRD>(p, i, j0, IPP, px, dirty, W, H); break;
+            case PM_CIRCLE: cmd_apply<PM_CIRCLE>(p, i, j0, IPP, px, dirty, W, H); break;
+            case PM_LINE: cmd_apply<PM_LINE>(p, i, j0, IPP, px, dirty, W, H); break;
+            case PM_TEX_FAST: cmd_apply<PM_TEX_FAST>(p, i, j0, IPP, px, dirty, W, H); break;
+            case PM_FILL: cmd_apply<PM_FILL>(p, i, j0, IPP, px, dirty, W, H); break;
+            default: cmd_apply<PM_SETPIX>(p, i, j0, IPP, px, dirty, W, H); break;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < CL_R; ++r) {
+        const i64 j = j0 + 4 * r;
+        if (!dirty[r] || i >= W || j >= H) continue;
+        f64* q = buf + (j * W + i) * IPP;
+        q[0] = px[r][0]; q[1] = px[r][1]; q[2] = px[r][2];
+        if (IPP == 4) q[3] = px[r][3];
+    }
+}
+
+struct CmdList {
+    std::vector<NrCmd> cmds;
+    NrCmd* dev = nullptr;
+    size_t devCap = 0;
+};
 
 static inline f64 dmin(f64 a, f64 b) { return (b < a) ? b : a; }   // std::min
 static inline f64 dmax(f64 a, f64 b) { return (a < b) ? b : a; }   // std::max
@@ -145,10 +261,19 @@ static PrimParams base_params(RenderContext* ctx) {
     return p;
 }
 
+static CmdList* cmd_list(RenderContext* ctx) {
+    if (!ctx->cmdList) ctx->cmdList = new CmdList();
+    return reinterpret_cast<CmdList*>(ctx->cmdList);
+}
+
 template <int MODE>
 static void launch(RenderContext* ctx, PrimParams& p, i64 i0, i64 i1, i64 j0, i64 j1) {
     if (i1 <= i0 || j1 <= j0) return;
     p.i0 = i0; p.j0 = j0; p.ni = i1 - i0; p.nj = j1 - j0;
+    if (ctx->recording) {   // queued; runs with the rest of the list
+        cmd_list(ctx)->cmds.push_back(NrCmd{MODE, p});
+        return;
+    }
     dim3 grid((unsigned)((p.ni + 63) / 64), (unsigned)((p.nj + 3) / 4));
     hipEvent_t e0, e1;
     nr_timing_begin(ctx, NRK_PRIM, &e0, &e1);
@@ -158,10 +283,27 @@ static void launch(RenderContext* ctx, PrimParams& p, i64 i0, i64 i1, i64 j0, i6
 }
 
 static void prepare(RenderContext* ctx) {
+    ctx->frameU8Valid = false;
+    if (ctx->recording) return;   // a pending clear is applied by the list launch
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize_color(ctx);
-    ctx->frameU8Valid = false;
 }
+
+// A texture that aliases a framebuffer (CreateTextureFromRenderContextShared)
+// is read as it is at the draw: a recorded draw would see it later, so such a
+// draw runs immediately, after the list recorded so far.
+struct ImmediateScope {
+    RenderContext* ctx;
+    bool was;
+    ImmediateScope(RenderContext* c, const Texture* tex) : ctx(c), was(c->recording) {
+        if (was && tex->aliasOf) {
+            NR_CHECK(hipSetDevice(ctx->device));
+            nr_flush_commands(ctx);
+            ctx->recording = false;
+        }
+    }
+    ~ImmediateScope() { ctx->recording = was; }
+};
 
 // Texture source for a draw.  An alias of the destination framebuffer is read
 // while being written in the reference (order-dependent result); here the
@@ -213,6 +355,7 @@ extern "C" {
 // cpp:720-779
 void DrawTexture(RenderContext* ctx, Texture* tex, f64 x, f64 y, f64 width, f64 height) {
     if (width == 0 || height == 0) return;
+    ImmediateScope imm(ctx, tex);
     prepare(ctx);
     PrimParams p = base_params(ctx);
     TexSrc src = tex_source(ctx, tex);
@@ -237,6 +380,7 @@ void DrawTexture(RenderContext* ctx, Texture* tex, f64 x, f64 y, f64 width, f64 
 void DrawSplittedTexture(RenderContext* ctx, Texture* tex, f64 x, f64 y, f64 width, f64 height, f64 uStart,
                          f64 uEnd, f64 vStart, f64 vEnd) {
     if (width == 0 || height == 0) return;
+    ImmediateScope imm(ctx, tex);
     prepare(ctx);
     PrimParams p = base_params(ctx);
     TexSrc src = tex_source(ctx, tex);
@@ -337,5 +481,120 @@ void DrawLine(RenderContext* ctx, f64 x1, f64 y1, f64 x2, f64 y2, f64 width, f64
     }
     launch<PM_LINE>(ctx, p, i0, i1, j0, j1);
 }
+
+}  // extern "C"
+
+// ---- deferred command list: host side ------------------------------------
+void nr_flush_commands(RenderContext* ctx) {
+    CmdList* L = reinterpret_cast<CmdList*>(ctx->cmdList);
+    if (!L || L->cmds.empty()) return;
+    const size_t n = L->cmds.size();
+    if (L->devCap < n) {
+        if (L->dev) NR_CHECK(hipFree(L->dev));
+        L->devCap = std::max(n, L->devCap * 2);
+        L->dev = nullptr;
+        if (hipMalloc((void**)&L->dev, L->devCap * sizeof(NrCmd)) != hipSuccess) {
+            nr_set_error_msg("command list: hipMalloc failed");
+            L->devCap = 0;
+            L->cmds.clear();
+            return;
+        }
+    }
+    // pageable source: the copy is staged before the call returns, so the
+    // vector can be reused at once
+    NR_CHECK(hipMemcpyAsync(L->dev, L->cmds.data(), n * sizeof(NrCmd), hipMemcpyHostToDevice, ctx->stream));
+    const int pend = ctx->pendColor ? 1 : 0;
+    const f64 pv = ctx->pendColorValue;
+    ctx->pendColor = false;   // the launch writes every pixel when a clear is pending
+    ctx->frameU8Valid = false;
+    if (ctx->width > 0 && ctx->height > 0) {
+        dim3 grid((unsigned)((ctx->width + CL_W - 1) / CL_W), (unsigned)((ctx->height + CL_H - 1) / CL_H));
+        hipEvent_t e0, e1;
+        nr_timing_begin(ctx, NRK_PRIM, &e0, &e1);
+        if (ctx->enableAlpha)
+            hipLaunchKernelGGL(k_cmd_list<4>, grid, dim3(64, 4), 0, ctx->stream, L->dev, (int)n, ctx->buffer,
+                               ctx->width, ctx->height, pend, pv);
+        else
+            hipLaunchKernelGGL(k_cmd_list<3>, grid, dim3(64, 4), 0, ctx->stream, L->dev, (int)n, ctx->buffer,
+                               ctx->width, ctx->height, pend, pv);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_PRIM, e0, e1);
+    }
+    L->cmds.clear();
+}
+
+void nr_drop_commands(RenderContext* ctx) {
+    CmdList* L = reinterpret_cast<CmdList*>(ctx->cmdList);
+    if (L) L->cmds.clear();
+}
+
+void nr_free_commands(RenderContext* ctx) {
+    CmdList* L = reinterpret_cast<CmdList*>(ctx->cmdList);
+    if (!L) return;
+    if (L->dev) {
+        NR_CHECK(hipStreamSynchronize(ctx->stream));   // a launch may still read it
+        NR_CHECK(hipFree(L->dev));
+    }
+    delete L;
+    ctx->cmdList = nullptr;
+}
+
+bool nr_record_fill(RenderContext* ctx, i64 i0, i64 i1, i64 j0, i64 j1, f64 r, f64 g, f64 b, f64 a) {
+    PrimParams p = base_params(ctx);
+    p.c[0] = r; p.c[1] = g; p.c[2] = b; p.c[3] = a;
+    launch<PM_FILL>(ctx, p, i0, i1, j0, j1);
+    return true;
+}
+
+bool nr_record_set_pixel(RenderContext* ctx, i64 x, i64 y, f64 r, f64 g, f64 b, f64 a) {
+    PrimParams p = base_params(ctx);
+    p.c[0] = r; p.c[1] = g; p.c[2] = b; p.c[3] = a;
+    p.x = (f64)x; p.y = (f64)y;
+    // RGB: the pixel whose channel 0 the reference's index+3 store hits (none
+    // past the end of the buffer)
+    i64 ox = x + 1, oy = y;
+    if (ox == ctx->width) { ox = 0; oy = y + 1; }
+    p.sx = (f64)ox; p.sy = (f64)(oy < ctx->height ? oy : -1);
+    if (ox == 0) launch<PM_SETPIX>(ctx, p, 0, ctx->width, y, std::min<i64>(y + 2, ctx->height));
+    else launch<PM_SETPIX>(ctx, p, x, x + 2, y, y + 1);
+    return true;
+}
+
+extern "C" {
+
+// Starts recording: primitive draws (DrawTexture, DrawSplittedTexture,
+// DrawRect, DrawLine, DrawCircle, DrawVerticalGrd, FillColor, ApplyPixel,
+// SetPixel) are queued and run together by EndCommandList (or by any call
+// that reads or otherwise touches the framebuffer), in recording order and
+// with the results of the immediate calls.  Transform and colour-transform
+// calls take effect as usual (each queued draw keeps the state it was
+// recorded with).  Replaces the reference's recording proxy
+// MultiThreadedVideoRenderContextPreparer (Pybind:302-367).
+void BeginCommandList(RenderContext* ctx) {
+    if (!ctx) return;
+    ctx->recording = true;
+}
+
+// Runs the queued draws (one launch) and stops recording.
+void EndCommandList(RenderContext* ctx) {
+    if (!ctx) return;
+    NR_CHECK(hipSetDevice(ctx->device));
+    nr_settle(ctx);
+    ctx->recording = false;
+}
+
+// Runs the queued draws and keeps recording (one frame of a recorded stream).
+void FlushCommandList(RenderContext* ctx) {
+    if (!ctx) return;
+    NR_CHECK(hipSetDevice(ctx->device));
+    nr_settle(ctx);
+}
+
+i64 GetCommandListLength(RenderContext* ctx) {
+    CmdList* L = ctx ? reinterpret_cast<CmdList*>(ctx->cmdList) : nullptr;
+    return L ? (i64)L->cmds.size() : 0;
+}
+
+bool IsRecordingCommands(RenderContext* ctx) { return ctx && ctx->recording; }
 
 }  // extern "C"

@@ -131,7 +131,10 @@ void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 
 
 using namespace nrtri;
 
-void nr_settle(RenderContext* ctx) { nrtri::settle(ctx); }
+void nr_settle(RenderContext* ctx) {
+    nrtri::settle(ctx);
+    nr_flush_commands(ctx);   // recorded draws come after the last batch in program order
+}
 
 extern "C" {
 

@@ -329,9 +329,62 @@ class RenderContext:
     def set_force_ordered_raster(self, on: bool = True):
         lib.SetForceOrderedRaster(self._ptr, on)
 
+    # ---- deferred command list (new) ---------------------
+    def begin_commands(self):
+        """Queue primitive draws until end_commands(): they then run as one
+        launch, in order, with the immediate calls' exact results."""
+        lib.BeginCommandList(self._ptr)
+
+    def end_commands(self):
+        lib.EndCommandList(self._ptr)
+
+    def flush_commands(self):
+        lib.FlushCommandList(self._ptr)
+
+    def command_list_length(self) -> int:
+        return lib.GetCommandListLength(self._ptr)
+
+    def is_recording(self) -> bool:
+        return bool(lib.IsRecordingCommands(self._ptr))
+
+    class _Commands:
+        def __init__(self, ctx):
+            self.ctx = ctx
+
+        def __enter__(self):
+            self.ctx.begin_commands()
+            return self.ctx
+
+        def __exit__(self, *exc):
+            self.ctx.end_commands()
+            return False
+
+    def commands(self):
+        """`with ctx.commands(): ...` records the block's draws as one list."""
+        return RenderContext._Commands(self)
+
     def set_pair_capacity_override(self, pairs: int):
         """Testing: cap the visibility raster's (tile, triangle) list (0 = auto)."""
         lib.SetPairCapacityOverride(self._ptr, pairs)
+
+
+class RecordingRenderContext(RenderContext):
+    """Counterpart of the reference's MultiThreadedVideoRenderContextPreparer
+    (Pybind:302-367): it records each frame's draw calls and replays them.
+    The reference's replay (`renderer`) is an unfinished stub and feeds a
+    VideoCap (FFmpeg, out of scope); here the recording is the library's
+    deferred command list and a frame's draws replay on the GPU as one launch
+    at end_of_frame().  Transform / state calls apply immediately, as in the
+    reference's `call_immediate_methods`."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.frames = 0
+        self.begin_commands()
+
+    def end_of_frame(self):
+        self.flush_commands()
+        self.frames += 1
 
 
 class Texture:

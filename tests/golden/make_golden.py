@@ -91,6 +91,8 @@ def ref_binding_scenes():
         "shapes_rgb": (scenes.scene_shapes, dict(alpha=False)),
         "clear_rgb": (scenes.scene_clear, dict(alpha=False)),
         "render_to_texture": (scenes.scene_render_to_texture, dict()),
+        "mix_rgb": scenes.all_scenes()["mix_rgb"],
+        "mix_rgba": scenes.all_scenes()["mix_rgba"],
     }
 
 

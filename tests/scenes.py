@@ -199,6 +199,18 @@ class GpuFactory:
         return self.R.Texture.from_numpy(arr)
 
 
+class GpuRecordingFactory(GpuFactory):
+    """The HIP library with every context recording from creation on: all
+    primitive draws of a scene go through the deferred command list and run
+    when a readback (or another flushing call) comes."""
+    name = "gpu-recording"
+
+    def context(self, w, h, alpha):
+        ctx = self.R.RenderContext(w, h, alpha)
+        ctx.begin_commands()
+        return ctx
+
+
 # ---------------------------------------------------------------------------
 # inputs
 # ---------------------------------------------------------------------------
@@ -379,6 +391,75 @@ def scene_demo(fac, t=0.37, size=64, alpha=True):
     return _out(ctx)
 
 
+def scene_primitive_mix(fac, W=96, H=72, alpha=False, n=160, seed=21, flushes=False, apply_px=True):
+    """A milrenderer-style frame (milrenderer.py:865-1038 mix): seeded random
+    sequence of every primitive under changing transforms, colour transforms
+    and saved states, with single-pixel ops.  flushes=True adds calls that
+    must run queued draws first (get_color, a framebuffer snapshot drawn
+    back) and a mid-sequence set_color.  apply_px=False leaves out
+    apply_pixel, which the reference binding cannot call (not exported,
+    SURVEY §8b)."""
+    r = np.random.Generator(np.random.PCG64(seed))
+    ctx = fac.context(W, H, alpha)
+    ctx.set_color(0.1, 0.1, 0.1, 0.1)
+    tex_a = fac.texture(pattern_u8(24, 20, 4, seed=seed + 1))
+    tex_b = fac.texture(pattern_u8(9, 13, 3, seed=seed + 2))
+    probes = []
+
+    def col():
+        return [float(v) for v in r.uniform(0, 1, 3)] + [float(r.choice([1.0, r.uniform(0.2, 0.9)]))]
+
+    for k in range(n):
+        op = int(r.integers(0, 13))
+        x, y = float(r.uniform(-10, W + 5)), float(r.uniform(-10, H + 5))
+        w, h = float(r.uniform(-3, W / 2)), float(r.uniform(-3, H / 2))
+        if op == 0:
+            ctx.draw_rect(x, y, w, h, *col())
+        elif op == 1:
+            ctx.draw_texture(tex_a if r.uniform() < 0.5 else tex_b, x, y, w, h)
+        elif op == 2:
+            ctx.draw_splitted_texture(tex_a, x, y, w, h, *[float(v) for v in r.uniform(0, 1, 4)])
+        elif op == 3:
+            ctx.draw_line(x, y, float(r.uniform(0, W)), float(r.uniform(0, H)), float(r.uniform(0.5, 6)), *col())
+        elif op == 4:
+            ctx.draw_circle(x, y, float(r.uniform(0.5, 15)), *col())
+        elif op == 5:
+            ctx.draw_vertical_grd(x, y, w, h, *col(), *col())
+        elif op == 6 and apply_px:
+            ctx.apply_pixel(int(r.integers(-2, W + 2)), int(r.integers(-2, H + 2)), *col())
+        elif op == 7:
+            px = int(r.integers(0, W)) if r.uniform() < 0.8 else W - 1
+            ctx.set_pixel(px, int(r.integers(0, H)), *col())
+        elif op == 8:
+            ctx.save_state()
+            ctx.translate(float(r.uniform(-20, 20)), float(r.uniform(-20, 20)))
+            ctx.rotate(float(r.uniform(-0.5, 0.5)))
+            ctx.scale(float(r.uniform(0.5, 1.5)), float(r.uniform(0.5, 1.5)))
+        elif op == 9:
+            ctx.restore_state()
+        elif op == 10:
+            ctx.apply_color_transform(*[float(v) for v in r.uniform(0.7, 1.1, 4)])
+        elif op == 11:
+            if r.uniform() < 0.2:
+                ctx.fill_color(*col())
+            else:
+                ctx.set_color_transform(1, 1, 1, 1)
+        elif op == 12 and flushes:
+            m = int(r.integers(0, 3))
+            if m == 0:
+                probes.append(ctx.get_color(float(r.uniform(0, W)), float(r.uniform(0, H))))
+            elif m == 1:
+                snap = ctx.as_texure()
+                ctx.draw_texture(snap, x, y, w, h)
+            else:
+                v = float(r.uniform(0, 1))
+                ctx.set_color(v, v, v, v)
+    out = _out(ctx)
+    if probes:
+        out["probes"] = np.array(probes, dtype=np.float64)
+    return out
+
+
 def scene_render_to_texture(fac, W=40, H=30):
     ctx = fac.context(W, H, True)
     ctx.set_color(0, 0, 0, 0)
@@ -505,6 +586,10 @@ BASIC_SCENES = {
     "demo_t037": (scene_demo, dict(t=0.37)),
     "demo_t081": (scene_demo, dict(t=0.81)),
     "render_to_texture": (scene_render_to_texture, dict()),
+    "mix_rgb": (scene_primitive_mix, dict(alpha=False, apply_px=False)),
+    "mix_rgba": (scene_primitive_mix, dict(alpha=True, seed=22, apply_px=False)),
+    "mix_px_flush_rgb": (scene_primitive_mix, dict(alpha=False, seed=23, flushes=True)),
+    "mix_px_flush_rgba": (scene_primitive_mix, dict(alpha=True, seed=24, flushes=True, n=220)),
     "u8": (scene_u8, dict()),
     "tri_edges": (scene_triangle_edges, dict()),
     "tri_multi": (scene_triangles_multi, dict()),

@@ -291,3 +291,19 @@ def test_pair_list_overflow_is_rerun_in_order(gpu, oracle):
         ctx.draw_triangles(xy[:200] + 3.5, c[:200], z=z[:200])
         outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
     assert_same(outs[0], outs[1], "overflow")
+
+
+def test_rotate_uses_sincos_like_the_reference_build(gpu, oracle):
+    """cpp:436-444 compiled by g++ -O3 (src/compile.sh) calls glibc sincos(),
+    which differs from separate sin/cos in the last bit for some angles: the
+    transform state after many rotations must equal the oracle's (gcc) bit
+    for bit."""
+    import numpy as np
+    r = np.random.Generator(np.random.PCG64(99))
+    g, o = gpu.context(8, 8, False), oracle.context(8, 8, False)
+    for a in r.uniform(-0.5, 0.5, 2000):
+        g.set_transform(1, 0, 0, 1, 0, 0)
+        o.set_transform(1, 0, 0, 1, 0, 0)
+        g.rotate(float(a))
+        o.rotate(float(a))
+        assert g.get_transform() == o.get_transform(), a

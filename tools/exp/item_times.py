@@ -37,13 +37,17 @@ nsl = ((info >> 32) & 0xFFFF).astype(np.int64)
 base = t0.min()
 s, e = (t0 - base) / 100.0, (t1 - base) / 100.0   # us
 dur = e - s
+tm = a[:, 3].astype(np.int64)
+mid = np.where(tm > 0, (tm - base) / 100.0, e)
+ras = mid - s          # item start -> raster barrier (key init + raster)
+sha = e - mid          # shading (+ split-tile merge)
 span = e.max()
 print(f"items {len(a)}  span {span:.1f} us  sum(dur) {dur.sum():.0f} us  mean concurrency {dur.sum() / span:.0f}")
 for lo, hi in ((0, 1), (1, 64), (64, 256), (256, 512), (512, 1025)):
     m = (ntri >= lo) & (ntri < hi) & (nsl <= 1)
     if m.any():
         print(f"  single tris [{lo},{hi}): n={m.sum():5d} dur mean {dur[m].mean():7.2f} max {dur[m].max():7.2f} us"
-              f"  us/tri {dur[m].sum() / max(1, ntri[m].sum()):.4f}")
+              f"  us/tri {dur[m].sum() / max(1, ntri[m].sum()):.4f}  raster {ras[m].mean():6.2f} shade {sha[m].mean():6.2f}")
 m = nsl > 1
 if m.any():
     print(f"  split slices: n={m.sum():5d} dur mean {dur[m].mean():7.2f} max {dur[m].max():7.2f} us"

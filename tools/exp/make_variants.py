@@ -21,20 +21,38 @@ VARIANTS = {
     "nst": ["EXP_NOF64ST", "EXP_NOU8ST"],
     "plant": ["EXP_PLANT"],
     "times": ["EXP_TIMES"],
+    "sht": ["EXP_SHT"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
 PATCHES = {
     "EXP_TIMES": [
         ("    for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {\n",
-         "    u64 exp_t0 = 0; u32 exp_prev = ~0u; u64 exp_info = 0;\n"
+         "    u64 exp_t0 = 0, exp_mid = 0; u32 exp_prev = ~0u; u64 exp_info = 0;\n"
          "    for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {\n"
          "        if (tid == 0) { const u64 now = __builtin_amdgcn_s_memrealtime();\n"
-         "            if (exp_prev != ~0u) exp_record(exp_prev, exp_t0, now, exp_info);\n"
+         "            if (exp_prev != ~0u) exp_record(exp_prev, exp_t0, now, exp_info, exp_mid);\n"
          "            exp_prev = item; exp_t0 = now; const uint4 dd = items[item];\n"
          "            exp_info = (u64)(dd.z - dd.y) | ((u64)dd.w << 32) | ((u64)blockIdx.x << 48); }\n"),
         ("    }   // work items\n",
          "    }   // work items\n"
-         "    if (tid == 0 && exp_prev != ~0u) exp_record(exp_prev, exp_t0, __builtin_amdgcn_s_memrealtime(), exp_info);\n"),
+         "    if (tid == 0 && exp_prev != ~0u) exp_record(exp_prev, exp_t0, __builtin_amdgcn_s_memrealtime(), exp_info, exp_mid);\n"),
+        ("        __syncthreads();\n        if (!multi) {   // the whole list was in this slice: shade now\n",
+         "        __syncthreads();\n        if (tid == 0) exp_mid = __builtin_amdgcn_s_memrealtime();\n"
+         "        if (!multi) {   // the whole list was in this slice: shade now\n"),
+    ],
+    "EXP_SHT": [   # shading phase durations summed over all shade_tile calls -> g_acc
+        ("    for (int i = tid; i < HTS; i += NT) ht[i] = 0;\n",
+         "    const u64 sh_t0 = __builtin_amdgcn_s_memrealtime();\n    for (int i = tid; i < HTS; i += NT) ht[i] = 0;\n"),
+        ("    __syncthreads();\n    // one record per staged winner",
+         "    __syncthreads();\n    const u64 sh_t1 = __builtin_amdgcn_s_memrealtime();\n    // one record per staged winner"),
+        ("    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    __syncthreads();\n",
+         "    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    __syncthreads();\n"
+         "    const u64 sh_t2 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("        store_pixel<ZMODE>(fp, gp, kv, cr, cg, cb, ca);\n    }\n}",
+         "        store_pixel<ZMODE>(fp, gp, kv, cr, cg, cb, ca);\n    }\n    __syncthreads();\n"
+         "    if (tid == 0) { const u64 sh_t3 = __builtin_amdgcn_s_memrealtime();\n"
+         "        atomicAdd(&g_acc[0], sh_t1 - sh_t0); atomicAdd(&g_acc[1], sh_t2 - sh_t1); atomicAdd(&g_acc[2], sh_t3 - sh_t2);\n"
+         "        atomicAdd(&g_acc[3], 1ull); atomicAdd(&g_acc[4], (u64)nU); }\n}"),
     ],
     "EXP_NOROWS": [
         ("            if (r0 >= r1) continue;\n",
@@ -85,11 +103,20 @@ PATCHES = {
 }
 PRELUDE = """#include <hip/hip_runtime.h>
 __device__ unsigned long long g_exp[4 * 65536];
-__device__ inline void exp_record(unsigned item, unsigned long long t0, unsigned long long t1, unsigned long long info) {
-    if (item < 65536) { g_exp[4 * item] = t0; g_exp[4 * item + 1] = t1; g_exp[4 * item + 2] = info; }
+__device__ unsigned long long g_acc[8];
+__device__ inline void exp_record(unsigned item, unsigned long long t0, unsigned long long t1, unsigned long long info,
+                                  unsigned long long tm = 0) {
+    if (item < 65536) { g_exp[4 * item] = t0; g_exp[4 * item + 1] = t1; g_exp[4 * item + 2] = info; g_exp[4 * item + 3] = tm; }
 }
 """
 HOST = """
+extern "C" int ExpGetAcc(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_acc), 64, 0, hipMemcpyDeviceToHost) == hipSuccess ? 8 : -1;
+}
+extern "C" int ExpResetAcc() {
+    unsigned long long z[8] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_acc), z, 64, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
 extern "C" int ExpGetItemTimes(unsigned long long* out, int n) {
     if (n > 4 * 65536) n = 4 * 65536;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;

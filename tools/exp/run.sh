@@ -4,6 +4,7 @@ mkdir -p gpurun_out
 cp libnativecpurenderer_amd/libNativeCPURenderer.so /tmp/keep.so
 for v in "$@"; do
   if [ "$v" = base ]; then cp /tmp/keep.so libnativecpurenderer_amd/libNativeCPURenderer.so; else cp tools/exp/$v.so libnativecpurenderer_amd/libNativeCPURenderer.so; fi
+  if [ "$v" = sht ]; then timeout -k 10 120 python tools/exp/shade_times.py; continue; fi
   if [ "$v" = plant ]; then timeout -k 10 120 python tools/exp/plan_times.py; continue; fi
   if [ "$v" = times ]; then
     timeout -k 10 300 python tools/exp/item_times.py > gpurun_out/exp_$v.log 2>&1; rc=$?; cat gpurun_out/exp_$v.log | tail -12
