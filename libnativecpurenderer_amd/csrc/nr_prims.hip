@@ -179,9 +179,34 @@ __global__ __launch_bounds__(256) void k_cmd_list(const NrCmd* __restrict__ cmds
             if (IPP == 4) px[r][3] = q[3];
         }
     }
-    for (int c = 0; c < ncmd; ++c) {
+    // the commands are taken 256 at a time: each thread tests one against the
+    // tile, and the hits are compacted in order (ballot + wave sums) into
+    // LDS, so the apply loop visits only the commands that touch the tile
+    __shared__ int sIdx[256];
+    __shared__ int sWave[4];
+    const int tid = threadIdx.y * 64 + threadIdx.x, lane = threadIdx.x, wave = threadIdx.y;
+    for (int base = 0; base < ncmd; base += 256) {
+        const int cidx = base + tid;
+        bool hit = false;
+        if (cidx < ncmd) {
+            const PrimParams& q = cmds[cidx].p;
+            hit = !(q.i0 >= tx0 + CL_W || q.i0 + q.ni <= tx0 || q.j0 >= ty0 + CL_H || q.j0 + q.nj <= ty0);
+        }
+        const unsigned long long m = __ballot(hit);
+        const int pre = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        if (lane == 0) sWave[wave] = (int)__builtin_popcountll(m);
+        __syncthreads();
+        int off = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            off += w < wave ? sWave[w] : 0;
+            total += sWave[w];
+        }
+        if (hit) sIdx[off + pre] = cidx;
+        __syncthreads();
+        for (int k = 0; k < total; ++k) {
+        const int c = __builtin_amdgcn_readfirstlane(sIdx[k]);
         const PrimParams& p = cmds[c].p;
-        if (p.i0 >= tx0 + CL_W || p.i0 + p.ni <= tx0 || p.j0 >= ty0 + CL_H || p.j0 + p.nj <= ty0) continue;
         switch (cmds[c].mode) {
             case PM_RECT: cmd_apply<PM_RECT>(p, i, j0, IPP, px, dirty, W, H); break;
             case PM_TEX: cmd_apply<PM_TEX>(p, i, j0, IPP, px, dirty, W, H); break;
@@ -193,6 +218,8 @@ __global__ __launch_bounds__(256) void k_cmd_list(const NrCmd* __restrict__ cmds
             case PM_FILL: cmd_apply<PM_FILL>(p, i, j0, IPP, px, dirty, W, H); break;
             default: cmd_apply<PM_SETPIX>(p, i, j0, IPP, px, dirty, W, H); break;
         }
+        }
+        __syncthreads();   // sIdx / sWave are reused by the next round
     }
 #pragma unroll
     for (int r = 0; r < CL_R; ++r) {

@@ -1,0 +1,126 @@
+"""milrenderer-style frame benchmark: the per-frame primitive
+mix of milrenderer.py:865-1038 (background texture, dim fill, gradient bands,
+judge lines with heads, tap/hold notes under per-note transforms, hit
+effects) at 1920x1080 RGB, synthetic textures and positions.  Times one
+frame drawn (a) with immediate calls (one launch per draw), (b) recorded as a
+deferred command list (one launch per frame), (c) by the CPU oracle (1
+thread); checks (b) against (c) bit for bit.  Prints one JSON line."""
+import argparse, json, math, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np
+import scenes
+
+W, H = 1920, 1080
+
+
+def make_textures(fac):
+    return dict(bg=fac.texture(scenes.pattern_u8(H, W, 3, seed=1)),
+                head=fac.texture(scenes.pattern_u8(64, 64, 4, seed=2)),
+                note=fac.texture(scenes.pattern_u8(32, 128, 4, seed=3)),
+                hold=fac.texture(scenes.pattern_u8(32, 96, 4, seed=4)),
+                hit=fac.texture(scenes.pattern_u8(256, 256, 4, seed=5)))
+
+
+def frame(ctx, tx, t, nlines=8, nnotes=300, nhits=40):
+    r = np.random.Generator(np.random.PCG64(1000 + int(t * 100)))
+    ctx.set_color(0, 0, 0, 0)
+    ctx.draw_texture(tx["bg"], 0, 0, W, H)
+    ctx.fill_color(0, 0, 0, 0.6)
+    ctx.draw_vertical_mut_grd(0, H * 0.6, W, H * 0.4, [(0.0, (0, 0, 0, 0)), (0.3, (0.1, 0.1, 0.2, 0.3)),
+                                                     (0.7, (0.1, 0.1, 0.3, 0.5)), (1.0, (0, 0, 0, 0.7))])
+    for k in range(nlines):
+        cx, cy = float(r.uniform(0.2 * W, 0.8 * W)), float(r.uniform(0.3 * H, 0.7 * H))
+        rot = float(r.uniform(-30, 30)) + 20 * math.sin(t + k)
+        ctx.save_state()
+        ctx.draw_texture(tx["head"], cx - 24, cy - 24, 48, 48)
+        ctx.restore_state()
+        dx, dy = math.cos(math.radians(rot)) * W, math.sin(math.radians(rot)) * W
+        ctx.draw_line(cx - dx, cy - dy, cx + dx, cy + dy, 4.0, 1, 1, 1, 0.8)
+        ctx.save_state()
+        ctx.translate(cx, cy)
+        ctx.rotate_degree(rot - 90)
+        for n in range(nnotes // nlines):
+            ctx.save_state()
+            ctx.translate(float(r.uniform(-400, 400)), float(r.uniform(-600, 0)))
+            ctx.rotate_degree(90)
+            ctx.scale(1.2, 1.2)
+            if n % 5:
+                ctx.draw_texture(tx["note"], -16, -64, 32, 128)
+            else:
+                L = float(r.uniform(60, 300))
+                ctx.draw_splitted_texture(tx["hold"], -20, -64, 21, 128, 0, 0.2, 0, 1)
+                ctx.draw_splitted_texture(tx["hold"], 0, -64, L + 1, 128, 0.2, 0.8, 0, 1)
+                ctx.draw_splitted_texture(tx["hold"], L, -64, 21, 128, 0.8, 1.0, 0, 1)
+            ctx.restore_state()
+        ctx.restore_state()
+    for k in range(nhits):
+        ctx.save_state()
+        ctx.translate(float(r.uniform(0, W)), float(r.uniform(0, H)))
+        ctx.rotate_degree(float(r.uniform(0, 360)))
+        ctx.apply_color_transform(1, 1, 1, float(r.uniform(0.3, 1)))
+        ctx.draw_texture(tx["hit"], -90, -90, 180, 180)
+        ctx.restore_state()
+
+
+class Counter:
+    """Counts the draw calls of a frame (no drawing)."""
+    def __init__(self): self.n = 0
+    def __getattr__(self, name):
+        def f(*a):
+            if name.startswith("draw") or name in ("fill_color", "set_color"): self.n += 1
+        return f
+    def draw_vertical_mut_grd(self, x, y, w, h, steps): self.n += len(steps) - 1
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=30)
+    ap.add_argument("--no-oracle", action="store_true")
+    args = ap.parse_args()
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    gpu = scenes.GpuFactory()
+    tx = make_textures(gpu)
+    cnt = Counter()
+    frame(cnt, {k: None for k in tx}, 0.0)
+    res = {"workload": "milrenderer-style frame 1920x1080 RGB", "draws_per_frame": cnt.n}
+    for mode in ("immediate", "recorded"):
+        ctx = R.RenderContext(W, H, False)
+        if mode == "recorded":
+            ctx.begin_commands()
+        for i in range(3):
+            frame(ctx, tx, i * 0.1)
+            ctx.flush_commands() if mode == "recorded" else None
+        ctx.flush()
+        t0 = time.perf_counter()
+        for i in range(args.frames):
+            frame(ctx, tx, i * 0.1)
+            if mode == "recorded":
+                ctx.flush_commands()
+        ctx.flush()
+        dt = (time.perf_counter() - t0) / args.frames
+        res[f"{mode}_ms_per_frame"] = round(dt * 1e3, 3)
+        if mode == "recorded":
+            ctx.enable_kernel_timing(True)
+            frame(ctx, tx, 0.5)
+            ctx.flush_commands()
+            ctx.flush()
+            tot, c = ctx.get_kernel_timing("prim")
+            res["recorded_launch_us"] = round(tot / max(c, 1) * 1e3, 1)
+            ctx.enable_kernel_timing(False)
+            frame(ctx, tx, 0.7)
+            g = ctx.get_buffer_numpy()
+    if not args.no_oracle:
+        of = scenes.OracleFactory()
+        otx = make_textures(of)
+        octx = of.context(W, H, False)
+        t0 = time.perf_counter()
+        frame(octx, otx, 0.7)
+        o = octx.get_buffer_numpy()
+        res["oracle_ms_per_frame"] = round((time.perf_counter() - t0) * 1e3, 1)
+        res["recorded_bit_exact_vs_oracle"] = bool(scenes.bits_equal(g, o))
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
