@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", action="store_true", help="also time c2/c5 and report them under 'extra'")
     ap.add_argument("--no-kernel-timing", action="store_true", help="time without per-kernel HIP events")
+    ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,6 +140,8 @@ def main():
     xy, z, c = make_scene(cfg)
     n_tri = len(xy)
     ctx = R.RenderContext(W, H, False)
+    if args.force_ordered:
+        ctx.set_force_ordered_raster(True)
     buf = R.TriangleBuffer(xy, c, z=z, gouraud=cfg["gouraud"])
     comm = None
     if world > 1:
