@@ -105,6 +105,7 @@ i64 GetFragmentCount(RenderContext* ctx);                                /* NEW 
 i64 GetLastRasterPath(RenderContext* ctx);                               /* NEW: 1 order-free, 2 ordered */
 void SetForceOrderedRaster(RenderContext* ctx, bool on);                 /* NEW: A/B and tests */
 void SetPairCapacityOverride(RenderContext* ctx, i64 pairs);             /* NEW: tests (0 = automatic) */
+void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW: k_vis variant 0 auto, 1 coop, 2 lane-only */
 
 /* ---- NEW: multi-GPU frames (tile-row sharding + RCCL assembly) */
 typedef struct NrComm NrComm;

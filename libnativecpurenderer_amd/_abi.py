@@ -79,6 +79,7 @@ DEVICE_ABI = {
     "GetLastRasterPath": (L, (P,)),
     "SetForceOrderedRaster": (None, (P, B)),
     "SetPairCapacityOverride": (None, (P, L)),
+    "SetCoopRaster": (None, (P, L)),
     "GetLastErrorString": (ctypes.c_char_p, ()),
     "ClearLastError": (None, ()),
     "SetDevice": (B, (L,)),

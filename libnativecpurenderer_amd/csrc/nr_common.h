@@ -54,7 +54,9 @@ struct TriScratch {
     u32* d_hplan = nullptr;                 // its device address
     u32 planSeq = 0;                        // sequence number of the last async plan
     u64 lastPairs = 0;                      // capacity estimate for the next batch
+    u64 lastN = 0;                          // its triangle count (k_vis variant choice)
     u64 capOverride = 0;                    // testing: force this pair capacity
+    int coopMode = 0;                       // k_vis variant: 0 auto, 1 coop, 2 lane-only (SetCoopRaster)
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
 };
 

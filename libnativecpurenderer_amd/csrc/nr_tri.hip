@@ -266,4 +266,9 @@ void SetPairCapacityOverride(RenderContext* ctx, i64 pairs) { ctx->tri.capOverri
 // New (testing / A-B measurement): force the ordered raster for every batch.
 void SetForceOrderedRaster(RenderContext* ctx, bool on) { ctx->forceOrdered = on ? 1 : 0; }
 
+// New (testing / A-B measurement): k_vis variant, 0 automatic (previous
+// batch's pair density), 1 with the wave-cooperative pass for large
+// triangles, 2 without it.
+void SetCoopRaster(RenderContext* ctx, i64 mode) { ctx->tri.coopMode = (int)(mode >= 0 && mode <= 2 ? mode : 0); }
+
 }  // extern "C"

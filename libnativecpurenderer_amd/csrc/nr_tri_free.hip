@@ -449,6 +449,35 @@ __device__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int 
     }
 }
 
+// Coverage-test + depth of one fragment into the tile's LDS keys (the
+// per-pixel step of both raster modes of k_vis; expressions as the oracle).
+template <int ZMODE>
+__device__ __forceinline__ void frag_key(u64* key, const u32* zin, int p, f64 X, f64 dy, f64 sx0, f64 e1x, f64 e1y,
+                                         f64 e2x, f64 e2y, f64 inv, f64 zz0, f64 dz1, f64 dz2, u64 id1) {
+    const f64 dx = X - sx0;
+    const f64 w1 = (dx * e2y - e2x * dy) * inv;
+    const f64 w2 = (e1x * dy - dx * e1y) * inv;
+    const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
+    const u32 zq = nr_quantize_depth_bl(zz);
+    if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
+    else if (zq < zin[p]) atomicMax(&key[p], id1);
+}
+
+__device__ __forceinline__ f64 readlane_f64(f64 v, int lane) {
+    const u64 b = __double_as_longlong(v);
+    const u32 lo = __builtin_amdgcn_readlane((u32)b, lane), hi = __builtin_amdgcn_readlane((u32)(b >> 32), lane);
+    return __longlong_as_double((long long)(((u64)hi << 32) | lo));
+}
+
+#ifndef NR_BIG_PX
+#define NR_BIG_PX 96
+#endif
+// A triangle whose bounding box covers at least BIG_PX pixels of the tile is
+// rasterised by the whole wave rather than by its own lane.
+constexpr int BIG_PX = NR_BIG_PX;
+static_assert(TH <= 64, "coop raster: one lane per tile row");
+constexpr f64 COOP_PAIRS = 2.0;
+
 constexpr int NW = VWG / 64;   // waves per k_vis workgroup
 constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 
@@ -460,7 +489,9 @@ constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 // then the lane walks the triangle's rows in this tile (exact span,
 // row_span_slopes) and their pixels (depth + LDS atomic on the packed key,
 // two pixels per step).  Then the workgroup shades the tile (shade_tile).
-template <int ZMODE, bool COUNT, bool GOURAUD>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+// COOP: large triangles rasterised by the whole wave (coop pass); the host picks it from the previous batch's
+// pair density -- the variant without it keeps fewer registers live for sliver meshes.
+template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES_PER_EU))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ vis, u32* __restrict__ done,
@@ -514,13 +545,19 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
 
         // this wave's chunks: c = wave, wave + NW, ...  One lane per triangle,
         // its setup in registers; the lane walks the triangle's rows in this
-        // tile (exact span from the per-edge slopes) and their pixels.
-        const u32 nch = (le - ls + 63) / 64;
+        // tile (exact span from the per-edge slopes) and their pixels.  A
+        // triangle covering many pixels of the tile is instead rasterised by
+        // the whole wave (coop_raster: lane = row for the spans, lane = column
+        // for the pixels).  A short slice is cut into NW chunks so that every
+        // wave gets a share.
+        const u32 ns = le - ls;
+        const u32 cs = (!COOP || ns >= 64u * NW) ? 64u : (ns + NW - 1) / NW;
+        const u32 nch = (ns + cs - 1) / cs;
         u32 pt = 0;
         f64 pxy[6], pz[3] = {0, 0, 0};
         auto prefetch = [&](u32 c) {
-            const u32 b = ls + c * 64 + lane;
-            if (c < nch && b < le) {
+            const u32 b = ls + c * cs + lane;
+            if (c < nch && (u32)lane < cs && b < le) {
                 pt = list[b];
                 load_tri_xy(fp.src.xy, pt, pxy);
                 if (DEPTH && fp.src.z) {
@@ -531,8 +568,8 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         };
         prefetch(wave);
         for (u32 c = wave; c < nch; c += NW) {
-            const u32 base = ls + c * 64;
-            const int cnt = (le - base) < 64u ? (int)(le - base) : 64;
+            const u32 base = ls + c * cs;
+            const int cnt = (int)((le - base) < cs ? (le - base) : cs);
             const u32 t = pt;
             f64 sx[3], sy[3], sl[3];
 #pragma unroll
@@ -542,45 +579,75 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
             const f64 den = e1x * e2y - e2x * e1y;
             int r0 = 0, r1 = 0;   // rows with a straddling edge: ymin <= y < ymax (exact)
+            bool big = false;
             if (lane < cnt && tri_finite(sx, sy) && den != 0) {
                 const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
                 r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
                 r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
+                const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
+                const f64 bw = fmin(xmx, (f64)x0 + wlim) - fmax(xmn, (f64)x0);   // bbox width in the tile
+                big = COOP && (f64)(r1 - r0) * bw >= (f64)BIG_PX;
             }
-            if (r0 >= r1) continue;
             edge_slopes(sx, sy, sl);
             const f64 inv = 1.0 / den;
             const u64 id1 = (u64)t + 1;
+            if (r0 < r1 && !big) {
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-            for (int r = r0; r < r1; ++r) {
-                const f64 y = (f64)(int)(y0 + r);
-                int xs, xe;
-                row_span_slopes(sx, sy, sl, y, (f64)x0, (f64)wlim, xs, xe);
-                if (COUNT) myFrags += (unsigned long long)(xe - xs);
-                if (xs >= xe) continue;
-                if (ZMODE == 0) {
+                for (int r = r0; r < r1; ++r) {
+                    const f64 y = (f64)(int)(y0 + r);
+                    int xs, xe;
+                    row_span_slopes(sx, sy, sl, y, (f64)x0, (f64)wlim, xs, xe);
+                    if (COUNT) myFrags += (unsigned long long)(xe - xs);
+                    if (xs >= xe) continue;
+                    if (ZMODE == 0) {
 #pragma clang loop vectorize(disable) interleave(disable)
-                    for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * KS + lx], id1);
-                    continue;
-                }
-                const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
-                auto frag = [&](int lx, f64 X) {
-                    const f64 dx = X - sx[0];
-                    const f64 w1 = (dx * e2y - e2x * dy) * inv;
-                    const f64 w2 = (e1x * dy - dx * e1y) * inv;
-                    const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
-                    const u32 zq = nr_quantize_depth_bl(zz);
-                    const int p = r * KS + lx;
-                    if (ZMODE == 1) atomicMin(&key[p], ((u64)zq << 32) | id1);
-                    else if (zq < zin[p]) atomicMax(&key[p], id1);
-                };
-                // two pixels per step: independent chains (ILP) and half the
-                // divergent trip count for the short spans of sliver triangles
-                f64 X = (f64)(int)(x0 + xs);   // pixel x as f64, exact (integers < 2^31)
+                        for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * KS + lx], id1);
+                        continue;
+                    }
+                    const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
+                    // two pixels per step: independent chains (ILP) and half the
+                    // divergent trip count for the short spans of sliver triangles
+                    f64 X = (f64)(int)(x0 + xs);   // pixel x as f64, exact (integers < 2^31)
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-                for (int lx = xs; lx < xe; lx += 2, X += 2.0) {
-                    frag(lx, X);
-                    if (lx + 1 < xe) frag(lx + 1, X + 1.0);
+                    for (int lx = xs; lx < xe; lx += 2, X += 2.0) {
+                        frag_key<ZMODE>(key, zin, r * KS + lx, X, dy, sx[0], e1x, e1y, e2x, e2y, inv, zz0, dz1, dz2,
+                                        id1);
+                        if (lx + 1 < xe)
+                            frag_key<ZMODE>(key, zin, r * KS + lx + 1, X + 1.0, dy, sx[0], e1x, e1y, e2x, e2y, inv,
+                                            zz0, dz1, dz2, id1);
+                    }
+                }
+            }
+            // the wave's large triangles, one at a time, all lanes on each
+            for (u64 bm = COOP ? __ballot(big && r0 < r1) : 0ull; bm; bm &= bm - 1) {
+                const int src = (int)__builtin_ctzll(bm);
+                f64 bx[3], by[3], bs[3];
+#pragma unroll
+                for (int v = 0; v < 3; ++v) {
+                    bx[v] = readlane_f64(sx[v], src);
+                    by[v] = readlane_f64(sy[v], src);
+                    bs[v] = readlane_f64(sl[v], src);
+                }
+                const f64 bi = readlane_f64(inv, src), bz0 = readlane_f64(zz0, src);
+                const f64 bd1 = readlane_f64(dz1, src), bd2 = readlane_f64(dz2, src);
+                const u64 bid = ((u64)__builtin_amdgcn_readlane((u32)(id1 >> 32), src) << 32) |
+                                (u64)__builtin_amdgcn_readlane((u32)id1, src);
+                const int br0 = __builtin_amdgcn_readlane(r0, src), br1 = __builtin_amdgcn_readlane(r1, src);
+                const f64 b1x = bx[1] - bx[0], b1y = by[1] - by[0], b2x = bx[2] - bx[0], b2y = by[2] - by[0];
+                // spans: lane l -> row br0 + l (at most TH <= 64 rows)
+                int lxs = 0, lxe = 0;
+                if (br0 + lane < br1) row_span_slopes(bx, by, bs, (f64)(int)(y0 + br0 + lane), (f64)x0, (f64)wlim, lxs, lxe);
+                if (COUNT) myFrags += (unsigned long long)(lxe - lxs);
+                const f64 X = (f64)(int)(x0 + lane);
+                for (int r = br0; r < br1; ++r) {
+                    const int xs = __builtin_amdgcn_readlane(lxs, r - br0), xe = __builtin_amdgcn_readlane(lxe, r - br0);
+                    if (lane < xs || lane >= xe) continue;
+                    if (ZMODE == 0) {
+                        atomicMax(&key[r * KS + lane], bid);
+                        continue;
+                    }
+                    const f64 dy = (f64)(int)(y0 + r) - by[0];
+                    frag_key<ZMODE>(key, zin, r * KS + lane, X, dy, bx[0], b1x, b1y, b2x, b2y, bi, bz0, bd1, bd2, bid);
                 }
             }
         }
@@ -634,7 +701,15 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
 
 template <int Z, bool C, bool G>
 void launch_vis(const FrameParams& fp, const TriScratch& sc, u32 grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_vis<Z, C, G>), dim3(grid), dim3(VWG), 0, s, fp, sc.fitems, sc.flist, sc.vis, sc.fdone,
+    // coop pass when the previous batch had more than COOP_PAIRS tiles per
+    // triangle (large triangles), or when there is no history
+    const bool coop = sc.coopMode ? sc.coopMode == 1
+                                  : (sc.lastN == 0 || sc.lastPairs > (u64)(COOP_PAIRS * (f64)sc.lastN));
+    if (coop)
+        hipLaunchKernelGGL((k_vis<Z, C, G, true>), dim3(grid), dim3(VWG), 0, s, fp, sc.fitems, sc.flist, sc.vis,
+                           sc.fdone, sc.dplan);
+    else
+        hipLaunchKernelGGL((k_vis<Z, C, G, false>), dim3(grid), dim3(VWG), 0, s, fp, sc.fitems, sc.flist, sc.vis, sc.fdone,
                        sc.dplan);
 }
 
@@ -744,6 +819,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         // grow both and bin again (the plan kernel re-zeroed the counters)
         NR_CHECK(hipStreamSynchronize(s));
         sc.lastPairs = sc.h_plan[0];
+        sc.lastN = (u64)src.n;
         grid = sc.h_plan[1];
         if (sc.h_plan[3]) break;
         if (attempt > 0 || !grow_list(sc.h_plan[0]) || !grow_items(sc.h_plan[1])) {
@@ -820,6 +896,7 @@ void settle(RenderContext* ctx) {
             std::this_thread::yield();
         }
     }
+    sc.lastN = (u64)pb->src.n;
     if (sc.h_plan[3]) {
         sc.lastPairs = sc.h_plan[0];
     } else {

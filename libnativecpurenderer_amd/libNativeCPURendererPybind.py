@@ -363,6 +363,11 @@ class RenderContext:
         """`with ctx.commands(): ...` records the block's draws as one list."""
         return RenderContext._Commands(self)
 
+    def set_coop_raster(self, mode: int):
+        """k_vis variant (testing / A-B): 0 automatic, 1 wave-cooperative
+        pass for large triangles, 2 lane-per-triangle only."""
+        lib.SetCoopRaster(self._ptr, mode)
+
     def set_pair_capacity_override(self, pairs: int):
         """Testing: cap the visibility raster's (tile, triangle) list (0 = auto)."""
         lib.SetPairCapacityOverride(self._ptr, pairs)

@@ -62,6 +62,32 @@ def test_c2_flat_depth_1080p(gpu, oracle):
     assert_same(g, o, "C2")
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_vis_variants_match_oracle(gpu, oracle, mode):
+    """Both k_vis variants (1: wave-cooperative pass for large triangles, 2:
+    lane per triangle only) on a soup mixing large and small triangles, in
+    every depth mode, RGB and RGBA."""
+    big = scenes.triangle_soup(300, 400, 300, 90, seed=41, gouraud=True)
+    small = scenes.triangle_soup(3000, 400, 300, 4, seed=42, gouraud=True)
+    xy = np.concatenate([big[0], small[0]]); z = np.concatenate([big[1], small[1]])
+    c = np.concatenate([big[2], small[2]])
+    perm = np.random.Generator(np.random.PCG64(43)).permutation(len(xy))
+    xy, z, c = xy[perm], z[perm], c[perm]
+    for depth, write in ((True, True), (True, False), (False, True)):
+        for alpha in (False, True):
+            outs = []
+            for fac in (gpu, oracle):
+                ctx = fac.context(400, 300, alpha)
+                if fac is gpu:
+                    ctx.set_coop_raster(mode)
+                ctx.set_color(0.25, 0.25, 0.25, 0.25)
+                ctx.set_depth_state(depth, write)
+                ctx.clear_depth()
+                ctx.draw_triangles(xy, c, z=z)
+                outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+            assert_same(outs[0], outs[1], f"mode={mode} depth={depth} write={write} alpha={alpha}")
+
+
 def test_c3_gouraud_depth_4k(gpu, oracle):
     xy, z, c = scenes.sphere_mesh(3840, 2160, 500, 1000)
     g, _ = _tri_frame(gpu, 3840, 2160, xy, z, c)

@@ -7,7 +7,7 @@ for v in "$@"; do
   if [ "$v" = sht ]; then timeout -k 10 120 python tools/exp/shade_times.py; continue; fi
   if [ "$v" = plant ]; then timeout -k 10 120 python tools/exp/plan_times.py; continue; fi
   if [ "$v" = times ]; then
-    timeout -k 10 300 python tools/exp/item_times.py > gpurun_out/exp_$v.log 2>&1; rc=$?; cat gpurun_out/exp_$v.log | tail -12
+    timeout -k 10 300 python tools/exp/item_times.py $ITEM_CFG > gpurun_out/exp_$v.log 2>&1; rc=$?; cat gpurun_out/exp_$v.log | tail -12
     [ $rc -eq 0 ] || break; continue
   fi
   timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline $BENCH_ARGS > gpurun_out/exp_$v.log 2>&1
