@@ -547,8 +547,8 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         // its setup in registers; the lane walks the triangle's rows in this
         // tile (exact span from the per-edge slopes) and their pixels.  A
         // triangle covering many pixels of the tile is instead rasterised by
-        // the whole wave (coop_raster: lane = row for the spans, lane = column
-        // for the pixels).  A short slice is cut into NW chunks so that every
+        // the whole wave (lane = row for the spans, then lane = (row, column) over
+        // blocks of rows sized to the widest span).  A short slice is cut into NW chunks so that every
         // wave gets a share.
         const u32 ns = le - ls;
         const u32 cs = (!COOP || ns >= 64u * NW) ? 64u : (ns + NW - 1) / NW;
@@ -638,16 +638,26 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
                 int lxs = 0, lxe = 0;
                 if (br0 + lane < br1) row_span_slopes(bx, by, bs, (f64)(int)(y0 + br0 + lane), (f64)x0, (f64)wlim, lxs, lxe);
                 if (COUNT) myFrags += (unsigned long long)(lxe - lxs);
-                const f64 X = (f64)(int)(x0 + lane);
-                for (int r = br0; r < br1; ++r) {
-                    const int xs = __builtin_amdgcn_readlane(lxs, r - br0), xe = __builtin_amdgcn_readlane(lxe, r - br0);
-                    if (lane < xs || lane >= xe) continue;
+                // pixels: blocks of R rows x C columns (C = the widest span
+                // rounded up to a power of two, R = 64 / C), lane -> (row, column)
+                int wmax = lxe - lxs;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) wmax = max(wmax, __shfl_xor(wmax, d, 64));
+                const int lc = wmax <= 8 ? 3 : wmax <= 16 ? 4 : wmax <= 32 ? 5 : 6;
+                const int nrows = br1 - br0, R = 64 >> lc;
+                for (int g = 0; g < nrows; g += R) {
+                    const int rl = g + (lane >> lc);
+                    const int xs = __shfl(lxs, rl & 63, 64), xe = __shfl(lxe, rl & 63, 64);
+                    const int lx = xs + (lane & ((1 << lc) - 1));
+                    if (rl >= nrows || lx >= xe) continue;
+                    const int r = br0 + rl;
                     if (ZMODE == 0) {
-                        atomicMax(&key[r * KS + lane], bid);
+                        atomicMax(&key[r * KS + lx], bid);
                         continue;
                     }
                     const f64 dy = (f64)(int)(y0 + r) - by[0];
-                    frag_key<ZMODE>(key, zin, r * KS + lane, X, dy, bx[0], b1x, b1y, b2x, b2y, bi, bz0, bd1, bd2, bid);
+                    frag_key<ZMODE>(key, zin, r * KS + lx, (f64)(int)(x0 + lx), dy, bx[0], b1x, b1y, b2x, b2y, bi, bz0,
+                                    bd1, bd2, bid);
                 }
             }
         }
