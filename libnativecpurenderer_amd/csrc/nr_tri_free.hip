@@ -38,8 +38,8 @@ namespace {
 #define NR_VWG 256
 #endif
 // k_vis occupancy: 4 waves per SIMD (<= 128 VGPRs, and LDS <= 40 KB per
-// workgroup through RMAX = 160) measured 6-10 % faster on C3 than 3 (135
-// VGPRs, 53.5 KB); k_vis is latency-bound, occupancy is its main lever.
+// workgroup: 280 shading records over the keys + NR_REC_EXTRA) measured 6-10 %
+// faster on C3 than 3 (135 VGPRs, 53.5 KB); k_vis is latency-bound.
 #ifndef NR_VIS_WAVES_PER_EU
 #define NR_VIS_WAVES_PER_EU 4
 #endif
@@ -271,11 +271,10 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 #ifndef NR_HTS
 #define NR_HTS 512
 #endif
-#ifndef NR_RMAX
-#define NR_RMAX 160
+#ifndef NR_REC_EXTRA   // LDS beyond the keys for shading records (k_vis stays <= 40 KB: 4 workgroups per CU)
+#define NR_REC_EXTRA 19200
 #endif
 constexpr int HTS = NR_HTS;    // hash slots (power of two)
-constexpr int RMAX = NR_RMAX;  // staged winner records per tile; later winners load directly
 constexpr int MAXPROBE = 16;   // linear-probe limit: a winner not placed / found within it loads directly
 
 template <bool GOURAUD>
@@ -284,41 +283,49 @@ struct ShadeStage {
     // flat record: rgb.  Alpha is not staged: every batch routed here has
     // vertex alpha 1 (and colourTransform[3] == 1), so the interpolated alpha
     // is 1 + 0*w1 + 0*w2, computed as such.
+    // LDS of a k_vis workgroup: hash table | dense-index table | keys | extra.
+    // The records of the shading pass overwrite the keys (each thread keeps
+    // its pixels' winners in registers by then) and run on into `extra`, so
+    // a tile stages RT records in KEY_BYTES + EXTRA bytes.
     static constexpr int REC = GOURAUD ? 16 : 3;
-    static constexpr int HT = 0, HIDX = HTS * 4, DIDX = HTS * 6, REC_OFF = ((HTS * 6 + RMAX * 4) + 15) & ~15;
-    static constexpr int BYTES = REC_OFF + RMAX * REC * 8;
+    static constexpr int KEY_BYTES = TH * (TW + 1) * 8;
+    static constexpr int EXTRA = GOURAUD ? NR_REC_EXTRA : 0;
+    static constexpr int RT_RAW = (KEY_BYTES + EXTRA) / (REC * 8);
+    static constexpr int RT = RT_RAW < TH * TW ? RT_RAW : TH * TW;   // staged records per tile
+    static constexpr int HT = 0, HIDX = HTS * 4, DIDX = HTS * 6;
+    static constexpr int KEY_OFF = ((DIDX + RT * 4) + 15) & ~15;
+    static constexpr int BYTES = KEY_OFF + KEY_BYTES + EXTRA;
 };
 
 __device__ __forceinline__ u32 ht_hash(u32 id) { return (id * 2654435761u) >> (32 - __builtin_ctz(HTS)); }
 
-// Pending clears for a pixel no fragment won.
+// Depth of a shaded pixel (winner kv; (u32)kv == 0: no fragment won it):
+// the winner's depth, or a pending depth clear.
 template <int ZMODE>
-__device__ __forceinline__ void store_clear(const FrameParams& fp, i64 p) {
-    if (fp.pendColor) {
-        const int ipp = fp.ipp;
-        f64* dst = fp.fb + p * ipp;
-        const f64 v = fp.pendColorValue;
-        dst[0] = v; dst[1] = v; dst[2] = v;
-        if (ipp == 4) dst[3] = v;
-        if (fp.frameU8) {
-            iu8* d8 = fp.frameU8 + p * ipp;
-            const iu8 v8 = nr_to_u8(v);
-            d8[0] = v8; d8[1] = v8; d8[2] = v8;
-            if (ipp == 4) d8[3] = v8;
-        }
-    }
-    if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+__device__ __forceinline__ void store_depth(const FrameParams& fp, i64 p, u64 kv) {
+    if (ZMODE == 1 && (u32)kv) fp.depth[p] = (u32)(kv >> 32);
+    else if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
 }
 
-// ApplyPixel (cpp:529-547) of the winner's colour, then framebuffer (+ u8
-// frame) and depth written once.  ca == 1 except for non-finite
-// barycentrics; the destination is read only then.
-template <int ZMODE>
-__device__ __forceinline__ void store_pixel(const FrameParams& fp, i64 p, u64 kv, f64 cr, f64 cg, f64 cb, f64 ca) {
+// Framebuffer (+ u8 frame) value of a pixel, written once.
+__device__ __forceinline__ void store_colour(const FrameParams& fp, i64 p, f64 cr, f64 cg, f64 cb, f64 ca) {
     const int ipp = fp.ipp;
     f64* dst = fp.fb + p * ipp;
+    dst[0] = cr; dst[1] = cg; dst[2] = cb;
+    if (ipp == 4) dst[3] = ca;
+    if (fp.frameU8) {
+        iu8* d8 = fp.frameU8 + p * ipp;
+        d8[0] = nr_to_u8(cr); d8[1] = nr_to_u8(cg); d8[2] = nr_to_u8(cb);
+        if (ipp == 4) d8[3] = nr_to_u8(ca);
+    }
+}
+
+// ApplyPixel (cpp:529-547) of the winner's colour.  ca == 1 except for
+// non-finite barycentrics; the destination is read only then.
+__device__ __forceinline__ void apply_winner(const FrameParams& fp, i64 p, f64& cr, f64& cg, f64& cb, f64& ca) {
     cr *= fp.ct[0]; cg *= fp.ct[1]; cb *= fp.ct[2]; ca *= fp.ct[3];
     if (ca != 1) {
+        const f64* dst = fp.fb + p * fp.ipp;
         f64 R, G, B;
         if (fp.pendColor) {
             R = G = B = fp.pendColorValue;
@@ -329,15 +336,16 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, i64 p, u64 kv
         cg = G * (1 - ca) + cg * ca;
         cb = B * (1 - ca) + cb * ca;
     }
-    dst[0] = cr; dst[1] = cg; dst[2] = cb;
-    if (ipp == 4) dst[3] = ca;
-    if (fp.frameU8) {
-        iu8* d8 = fp.frameU8 + p * ipp;
-        d8[0] = nr_to_u8(cr); d8[1] = nr_to_u8(cg); d8[2] = nr_to_u8(cb);
-        if (ipp == 4) d8[3] = nr_to_u8(ca);
+}
+
+// Pending clears of a pixel no fragment won.
+template <int ZMODE>
+__device__ __forceinline__ void store_clear(const FrameParams& fp, i64 p) {
+    if (fp.pendColor) {
+        const f64 v = fp.pendColorValue;
+        store_colour(fp, p, v, v, v, v);
     }
-    if (ZMODE == 1) fp.depth[p] = (u32)(kv >> 32);
-    else if (ZMODE == 2 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+    store_depth<ZMODE>(fp, p, 0);
 }
 
 // Shading record of triangle t (the expressions of the per-pixel path, once).
@@ -380,24 +388,39 @@ __device__ __forceinline__ void record_colour(const f64* r, i64 px, i64 py, f64&
     }
 }
 
-// Shades the tile from its LDS keys (key(p) for tile pixel p = ly*TW + lx).
-template <int ZMODE, bool GOURAUD, int NT, typename KeyFn>
-__device__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int hlim, KeyFn key, unsigned char* smem,
-                           u32& nU) {
+// Shades the tile from its LDS keys (`key` at row stride KS).  Pass 1: each
+// thread takes its PPT pixels (p = tid + k*NT), stores their depth, keeps
+// their winners in registers and enters the distinct winners in an LDS hash
+// table (dense index d).  Pass 2: one record per staged winner (independent
+// global loads: one latency round), written over the keys.  Pass 3: colour,
+// ApplyPixel, framebuffer (+ u8 frame) written once.  A winner past the RT
+// staged records (or not placed within MAXPROBE probes) loads its own record.
+template <int ZMODE, bool GOURAUD, int NT>
+__device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int hlim,
+                                           const u64* key, unsigned char* lds, u32& nU) {
     using St = ShadeStage<GOURAUD>;
-    u32* ht = reinterpret_cast<u32*>(smem + St::HT);
-    unsigned short* hidx = reinterpret_cast<unsigned short*>(smem + St::HIDX);
-    u32* didx = reinterpret_cast<u32*>(smem + St::DIDX);
-    f64* rec = reinterpret_cast<f64*>(smem + St::REC_OFF);
+    constexpr int PPT = TH * TW / NT;
+    u32* ht = reinterpret_cast<u32*>(lds + St::HT);
+    unsigned short* hidx = reinterpret_cast<unsigned short*>(lds + St::HIDX);
+    u32* didx = reinterpret_cast<u32*>(lds + St::DIDX);
+    f64* rec = reinterpret_cast<f64*>(lds + St::KEY_OFF);   // over the keys, after pass 1
     const int tid = threadIdx.x;
-    auto valid = [&](int p) { return (p & (TW - 1)) < wlim && p / TW < hlim; };
     for (int i = tid; i < HTS; i += NT) ht[i] = 0;
     if (tid == 0) nU = 0;
     __syncthreads();
-    // distinct winners -> dense indices
-    for (int p = tid; p < TH * TW; p += NT) {
-        if (!valid(p)) continue;
-        const u32 id = (u32)key(p);
+    u32 ids[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) ids[k] = 0;
+#pragma unroll 1
+    for (int k = 0; k < PPT; ++k) {
+        const int p = tid + k * NT, lx = p & (TW - 1), ly = p / TW;
+        if (lx >= wlim || ly >= hlim) continue;
+        const u64 kv = key[ly * (TW + 1) + lx];
+        const u32 id = (u32)kv;
+#pragma unroll
+        for (int q = 0; q < PPT; ++q)
+            if (q == k) ids[q] = id;   // static register index
+        store_depth<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx, kv);
         if (!id) continue;
         u32 h = ht_hash(id);
         for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
@@ -407,30 +430,36 @@ __device__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int 
                 const u32 old = atomicCAS(&ht[h], 0u, id);
                 if (old == 0) {
                     const u32 d = atomicAdd(&nU, 1u);
-                    hidx[h] = (unsigned short)(d < RMAX ? d : RMAX);
-                    if (d < RMAX) didx[d] = id;
+                    hidx[h] = (unsigned short)(d < (u32)St::RT ? d : St::RT);
+                    if (d < (u32)St::RT) didx[d] = id;
                     break;
                 }
                 if (old == id) break;
             }
         }
     }
-    __syncthreads();
-    // one record per staged winner (independent loads: one latency round)
-    const u32 U = nU < (u32)RMAX ? nU : (u32)RMAX;
+    __syncthreads();   // every key read: the records may overwrite them
+    const u32 U = nU < (u32)St::RT ? nU : (u32)St::RT;
     for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);
     __syncthreads();
-    for (int p = tid; p < TH * TW; p += NT) {
-        if (!valid(p)) continue;
-        const i64 px = x0 + (p & (TW - 1)), py = y0 + p / TW;
+#pragma unroll 1
+    for (int k = 0; k < PPT; ++k) {
+        const int p = tid + k * NT, lx = p & (TW - 1), ly = p / TW;
+        if (lx >= wlim || ly >= hlim) continue;
+        const i64 px = x0 + lx, py = y0 + ly;
         const i64 gp = py * fp.W + px;
-        const u64 kv = key(p);
-        const u32 id = (u32)kv;
+        u32 id = 0;
+#pragma unroll
+        for (int q = 0; q < PPT; ++q)
+            if (q == k) id = ids[q];
         if (!id) {
-            store_clear<ZMODE>(fp, gp);
+            if (fp.pendColor) {
+                const f64 v = fp.pendColorValue;
+                store_colour(fp, gp, v, v, v, v);
+            }
             continue;
         }
-        int d = RMAX;
+        int d = St::RT;
         u32 h = ht_hash(id);
         for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
             const u32 cur = ht[h];
@@ -438,14 +467,15 @@ __device__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int 
             if (cur == 0) break;
         }
         f64 cr, cg, cb, ca;
-        if (d < RMAX) {
+        if (d < St::RT) {
             record_colour<GOURAUD>(rec + d * St::REC, px, py, cr, cg, cb, ca);
         } else {   // overflow: load this pixel's winner directly
             f64 r[St::REC];
             make_record<GOURAUD>(fp, (i64)id - 1, r);
             record_colour<GOURAUD>(r, px, py, cr, cg, cb, ca);
         }
-        store_pixel<ZMODE>(fp, gp, kv, cr, cg, cb, ca);
+        apply_winner(fp, gp, cr, cg, cb, ca);
+        store_colour(fp, gp, cr, cg, cb, ca);
     }
 }
 
@@ -499,10 +529,11 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
     constexpr bool DEPTH = ZMODE != 0;
     // tile keys, rows padded to KS = 65 entries: lanes working on different
     // rows at the same column then hit different LDS banks
-    __shared__ u64 key[TH * KS];
+    // one LDS block (ShadeStage): hash tables | tile keys | extra; the
+    // shading records overwrite the keys
+    __shared__ __attribute__((aligned(16))) unsigned char lds[ShadeStage<GOURAUD>::BYTES];
+    u64* const key = reinterpret_cast<u64*>(lds + ShadeStage<GOURAUD>::KEY_OFF);
     __shared__ u32 zin[ZMODE == 2 ? TH * KS : 1];
-    // shading staging (ShadeStage)
-    __shared__ __attribute__((aligned(16))) unsigned char smem[ShadeStage<GOURAUD>::BYTES];
     __shared__ u32 nU;
     __shared__ int sLast;
     __shared__ unsigned long long sFrag;
@@ -663,8 +694,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         }
         __syncthreads();
         if (!multi) {   // the whole list was in this slice: shade now
-            shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim,
-                                            [&](int p) { return key[(p / TW) * KS + (p & (TW - 1))]; }, smem, nU);
+            shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim, key, lds, nU);
             continue;
         }
         // split tile: merge into the global keys; the last slice to finish
@@ -698,8 +728,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
             __hip_atomic_store(g, ZMODE == 1 ? ~0ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim,
-                                        [&](int p) { return key[(p / TW) * KS + (p & (TW - 1))]; }, smem, nU);
+        shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim, key, lds, nU);
     }   // work items
     if (COUNT) {
         __syncthreads();
