@@ -51,6 +51,9 @@ void ClearLastError() {
 // contexts and textures of that device, so cross-object ordering (texture
 // uploads, render-to-texture) is the reference's single-threaded order.
 // ---------------------------------------------------------------------------
+#ifndef NR_MAIN_PRIO
+#define NR_MAIN_PRIO 1   // main stream at the greatest priority
+#endif
 static std::mutex g_dev_mu;
 static std::vector<hipStream_t> g_streams;
 
@@ -59,9 +62,26 @@ hipStream_t nr_stream_for(int device) {
     if ((int)g_streams.size() <= device) g_streams.resize(device + 1, nullptr);
     if (!g_streams[device]) {
         NR_CHECK(hipSetDevice(device));
-        NR_CHECK(hipStreamCreateWithFlags(&g_streams[device], hipStreamNonBlocking));
+        int least = 0, greatest = 0;
+        NR_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        NR_CHECK(hipStreamCreateWithPriority(&g_streams[device], hipStreamNonBlocking, NR_MAIN_PRIO ? greatest : least));
     }
     return g_streams[device];
+}
+
+static std::vector<hipStream_t> g_bin_streams;
+hipStream_t nr_bin_stream_for(int device) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if ((int)g_bin_streams.size() <= device) g_bin_streams.resize(device + 1, nullptr);
+    if (!g_bin_streams[device]) {
+        // lowest priority: the next batch's binning fills the gaps the
+        // current raster leaves instead of competing with it
+        NR_CHECK(hipSetDevice(device));
+        int least = 0, greatest = 0;
+        NR_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        NR_CHECK(hipStreamCreateWithPriority(&g_bin_streams[device], hipStreamNonBlocking, least));
+    }
+    return g_bin_streams[device];
 }
 
 // live contexts (nr_settle_all validates every pending batch)
@@ -242,18 +262,23 @@ static hipEvent_t ev_get(RenderContext* ctx) {
     return e;
 }
 
-void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b) {
+void nr_timing_begin_on(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b, hipStream_t s) {
     *a = *b = nullptr;
     if (!ctx->timing || !((ctx->timingMask >> kid) & 1ull)) return;
     *a = ev_get(ctx);
     *b = ev_get(ctx);
-    NR_CHECK(hipEventRecord(*a, ctx->stream));
+    NR_CHECK(hipEventRecord(*a, s));
 }
-
-void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b) {
+void nr_timing_end_on(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b, hipStream_t s) {
     if (!ctx->timing || !a) return;
-    NR_CHECK(hipEventRecord(b, ctx->stream));
+    NR_CHECK(hipEventRecord(b, s));
     ctx->evPending.push_back({kid, {a, b}});
+}
+void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b) {
+    nr_timing_begin_on(ctx, kid, a, b, ctx->stream);
+}
+void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b) {
+    nr_timing_end_on(ctx, kid, a, b, ctx->stream);
 }
 
 static void timing_collect(RenderContext* ctx) {
@@ -324,14 +349,22 @@ void DestroyRenderContext(RenderContext* ctx) {
             if (g_ctxs[i] == ctx) { g_ctxs.erase(g_ctxs.begin() + i); break; }
     }
     NR_CHECK(hipStreamSynchronize(ctx->stream));
+    NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
                     t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
-                    t.fcnt,      t.foff,       t.fitems,   t.fcur, t.fdone, t.frect, t.flist, t.vis,  t.dplan, ctx->frameU8};
+                    t.fdone,     t.vis,        ctx->frameU8};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
+    for (auto& F : t.fset) {
+        void* fp[] = {F.fcnt, F.foff, F.fcur, F.fitems, F.frect, F.flist, F.dplan};
+        for (void* p : fp)
+            if (p) NR_CHECK(hipFree(p));
+        if (F.h_plan) NR_CHECK(hipHostFree(F.h_plan));
+        if (F.evBin) NR_CHECK(hipEventDestroy(F.evBin));
+        if (F.evVis) NR_CHECK(hipEventDestroy(F.evVis));
+    }
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));
-    if (t.h_plan) NR_CHECK(hipHostFree(t.h_plan));
     for (auto& p : ctx->evPending) {
         NR_CHECK(hipEventDestroy(p.second.first));
         NR_CHECK(hipEventDestroy(p.second.second));

@@ -43,15 +43,24 @@ struct TriScratch {
     u64* h_total = nullptr;                 // pinned readback: [0] pairs, [1] last count, [2] fragments
     u64* d_frag = nullptr;                  // device fragment counter
     u32* d_flag = nullptr;                  // device non-opaque flag
-    // visibility-buffer raster (nr_tri_free.hip)
-    u32* fcnt = nullptr; u32* foff = nullptr; u32* fcur = nullptr; u32* fdone = nullptr; size_t ftile_cap = 0;
-    uint4* fitems = nullptr; size_t fitems_cap = 0;
-    u64* frect = nullptr; size_t frect_cap = 0;   // per-triangle tile rectangle (count -> emit)
-    u32* flist = nullptr; size_t flist_cap = 0;
+    // visibility-buffer raster (nr_tri_free.hip).  The binning outputs are
+    // double-buffered (FreeSet): a batch drawn from a TriangleBuffer is binned
+    // on the device's binning stream while the previous batch's k_vis runs.
+    struct FreeSet {
+        u32* fcnt = nullptr; u32* foff = nullptr; u32* fcur = nullptr; size_t ftile_cap = 0;
+        uint4* fitems = nullptr; size_t fitems_cap = 0;
+        u64* frect = nullptr; size_t frect_cap = 0;   // per-triangle tile rectangle (count -> emit)
+        u32* flist = nullptr; size_t flist_cap = 0;
+        u32* dplan = nullptr;
+        u32* h_plan = nullptr;              // pinned, device-mapped copy of the plan totals
+        u32* d_hplan = nullptr;             // its device address
+        hipEvent_t evBin = nullptr;         // binning done (binning stream)
+        hipEvent_t evVis = nullptr;         // k_vis done reading the set (main stream)
+        bool visRecorded = false;
+    } fset[2];
+    int fnext = 0;                          // set of the next batch
+    u32* fdone = nullptr; size_t fdone_cap = 0;   // split-tile slice counters (k_vis only)
     u64* vis = nullptr; size_t vis_cap = 0; int visNeutral = -1;
-    u32* dplan = nullptr;
-    u32* h_plan = nullptr;                  // pinned, device-mapped copy of the plan totals
-    u32* d_hplan = nullptr;                 // its device address
     u32 planSeq = 0;                        // sequence number of the last async plan
     u64 lastPairs = 0;                      // capacity estimate for the next batch
     u64 lastN = 0;                          // its triangle count (k_vis variant choice)
@@ -130,6 +139,9 @@ struct TriangleBuffer {
 
 // host helpers shared across translation units
 hipStream_t nr_stream_for(int device);
+hipStream_t nr_bin_stream_for(int device);        // second stream: triangle binning overlapped with the raster
+void nr_timing_begin_on(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b, hipStream_t s);
+void nr_timing_end_on(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b, hipStream_t s);
 void nr_materialize(RenderContext* ctx);          // flush pending clears
 void nr_materialize_color(RenderContext* ctx);
 void nr_materialize_depth(RenderContext* ctx);

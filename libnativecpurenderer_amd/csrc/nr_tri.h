@@ -261,7 +261,7 @@ void finish_batch(RenderContext* ctx, const FrameParams& fp);
 
 // the two rasterisers (host side)
 void draw_ordered(RenderContext* ctx, const TriSrc& src);
-void draw_free(RenderContext* ctx, const TriSrc& src);
+void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable);   // immutable: binning may overlap the previous raster
 void settle(RenderContext* ctx);
 
 }  // namespace nrtri

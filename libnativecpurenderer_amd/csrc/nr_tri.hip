@@ -114,7 +114,8 @@ Opacity device_opacity(RenderContext* ctx, const TriSrc& src) {
     return *h ? OPQ_BLENDED : OPQ_OPAQUE;
 }
 
-void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud, Opacity opq) {
+void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud, Opacity opq,
+          bool immutable = false) {
     NR_CHECK(hipSetDevice(ctx->device));
     settle(ctx);
     if (n <= 0 || ctx->width <= 0 || ctx->height <= 0) return;
@@ -122,7 +123,7 @@ void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 
     TriSrc src{xy, z, rgba, gouraud ? 1 : 0, n};
     const bool freeEligible = ctx->ct[3] == 1 && ctx->forceOrdered == 0;
     if (freeEligible && opq == OPQ_UNKNOWN) opq = device_opacity(ctx, src);
-    if (freeEligible && opq == OPQ_OPAQUE) draw_free(ctx, src);
+    if (freeEligible && opq == OPQ_OPAQUE) draw_free(ctx, src, immutable);
     else draw_ordered(ctx, src);
 }
 
@@ -244,7 +245,8 @@ void DestroyTriangleBuffer(TriangleBuffer* tb) {
 i64 GetTriangleBufferCount(TriangleBuffer* tb) { return tb->n; }
 
 void DrawTriangleBuffer(RenderContext* ctx, TriangleBuffer* tb) {
-    draw(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud, tb->opaque ? OPQ_OPAQUE : OPQ_BLENDED);
+    // a TriangleBuffer never changes: its binning may overlap the previous batch's raster
+    draw(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud, tb->opaque ? OPQ_OPAQUE : OPQ_BLENDED, true);
 }
 
 // New: count covered on-screen pixel x triangle pairs (the "shaded+Z-tested

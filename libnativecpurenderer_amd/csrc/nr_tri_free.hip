@@ -739,23 +739,24 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
 }
 
 template <int Z, bool C, bool G>
-void launch_vis(const FrameParams& fp, const TriScratch& sc, u32 grid, hipStream_t s) {
+void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid, hipStream_t s) {
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
     const bool coop = sc.coopMode ? sc.coopMode == 1
                                   : (sc.lastN == 0 || sc.lastPairs > (u64)(COOP_PAIRS * (f64)sc.lastN));
     if (coop)
-        hipLaunchKernelGGL((k_vis<Z, C, G, true>), dim3(grid), dim3(VWG), 0, s, fp, sc.fitems, sc.flist, sc.vis,
-                           sc.fdone, sc.dplan);
+        hipLaunchKernelGGL((k_vis<Z, C, G, true>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
+                           sc.fdone, F.dplan);
     else
-        hipLaunchKernelGGL((k_vis<Z, C, G, false>), dim3(grid), dim3(VWG), 0, s, fp, sc.fitems, sc.flist, sc.vis, sc.fdone,
-                       sc.dplan);
+        hipLaunchKernelGGL((k_vis<Z, C, G, false>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
+                           sc.fdone, F.dplan);
 }
 
 template <int Z, bool G>
-void launch_vis_z(const FrameParams& fp, const TriScratch& sc, u32 grid, hipStream_t s) {
-    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, grid, s);
-    else launch_vis<Z, false, G>(fp, sc, grid, s);
+void launch_vis_z(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid,
+                  hipStream_t s) {
+    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, F, grid, s);
+    else launch_vis<Z, false, G>(fp, sc, F, grid, s);
 }
 
 // Everything a batch needs to be re-run after an overflow (nr_settle).
@@ -763,33 +764,59 @@ struct PendingBatch {
     TriSrc src;
     FrameParams fp;
     BinParams bp;
+    int set;
+    u32 seq;
 };
 
-// Enqueues one batch.  exact: read the pair/item totals back (host sync) and
-// allocate exactly; otherwise size the list from `cap`, let the plan kernel
-// check it on the device and validate later (nr_settle).
+static hipEvent_t sync_event() {
+    hipEvent_t e;
+    NR_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+    return e;
+}
+
+// Enqueues one batch with binning outputs in set `si`.  exact: read the
+// pair/item totals back (host sync) and allocate exactly; otherwise size the
+// list from the previous batch, let the plan kernel check it on the device
+// and validate later (nr_settle).  pipelined: bin on the device's binning
+// stream -- after the raster that last read set `si`, not after everything
+// queued before on the main stream -- so that it overlaps the previous
+// batch's k_vis (only for immutable inputs: a TriangleBuffer).
 static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
-                         bool exact) {
-    hipStream_t s = ctx->stream;
+                         bool exact, int si, bool pipelined, u32* seqOut) {
+    hipStream_t sa = ctx->stream;
+    hipStream_t sb = pipelined ? nr_bin_stream_for(ctx->device) : sa;
     TriScratch& sc = ctx->tri;
+    TriScratch::FreeSet& F = sc.fset[si];
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
     const bool g = src.gouraud != 0;
+    if (!F.evBin) { F.evBin = sync_event(); F.evVis = sync_event(); }
+    // the set's buffers are rewritten (binning stream) only after the raster
+    // that last read them; a regrow frees them, so the host waits for it then
+    if (F.visRecorded && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, F.evVis, 0));
+    auto quiesce = [&]() {
+        if (F.visRecorded) NR_CHECK(hipEventSynchronize(F.evVis));
+    };
 
-    u32* tb[4] = {sc.fcnt, sc.foff, sc.fcur, sc.fdone};
-    const size_t oldcap = sc.ftile_cap;
-    if (!grow_set(tb, &sc.ftile_cap, (size_t)ntiles + 1)) return false;
-    sc.fcnt = tb[0]; sc.foff = tb[1]; sc.fcur = tb[2]; sc.fdone = tb[3];
-    if (sc.ftile_cap != oldcap) {   // counters start at zero; k_free_plan re-zeroes them after each use
-        NR_CHECK(hipMemsetAsync(sc.fcnt, 0, sc.ftile_cap * sizeof(u32), s));
-        NR_CHECK(hipMemsetAsync(sc.fcur, 0, sc.ftile_cap * sizeof(u32), s));
-        NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.ftile_cap * sizeof(u32), s));
+    if (F.ftile_cap < (size_t)ntiles + 1 || !F.fcnt) quiesce();
+    u32* tb[3] = {F.fcnt, F.foff, F.fcur};
+    const size_t oldcap = F.ftile_cap;
+    if (!grow_set(tb, &F.ftile_cap, (size_t)ntiles + 1)) return false;
+    F.fcnt = tb[0]; F.foff = tb[1]; F.fcur = tb[2];
+    if (F.ftile_cap != oldcap) {   // counters start at zero; k_free_plan re-zeroes them after each use
+        NR_CHECK(hipMemsetAsync(F.fcnt, 0, F.ftile_cap * sizeof(u32), sb));
+        NR_CHECK(hipMemsetAsync(F.fcur, 0, F.ftile_cap * sizeof(u32), sb));
     }
-    if (!sc.dplan) NR_CHECK(hipMalloc(&sc.dplan, 4 * sizeof(u32)));
-    if (!sc.h_plan) {
-        NR_CHECK(hipHostMalloc((void**)&sc.h_plan, 8 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
-        sc.h_plan[4] = 0;
-        NR_CHECK(hipHostGetDevicePointer((void**)&sc.d_hplan, sc.h_plan, 0));
+    u32* db[1] = {sc.fdone};
+    const size_t olddone = sc.fdone_cap;
+    if (!grow_set(db, &sc.fdone_cap, (size_t)ntiles + 1)) return false;
+    sc.fdone = db[0];
+    if (sc.fdone_cap != olddone) NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.fdone_cap * sizeof(u32), sa));
+    if (!F.dplan) NR_CHECK(hipMalloc(&F.dplan, 4 * sizeof(u32)));
+    if (!F.h_plan) {
+        NR_CHECK(hipHostMalloc((void**)&F.h_plan, 8 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
+        F.h_plan[4] = 0;
+        NR_CHECK(hipHostGetDevicePointer((void**)&F.d_hplan, F.h_plan, 0));
     }
     u64* vb[1] = {sc.vis};
     const size_t oldvis = sc.vis_cap;
@@ -799,36 +826,41 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     // neutral value of its depth mode; refill only when the mode changes
     const int neutral = zmode == 1 ? 1 : 0;
     if (sc.vis_cap != oldvis || sc.visNeutral != neutral) {
-        NR_CHECK(hipMemsetD32Async((hipDeviceptr_t)sc.vis, neutral ? 0xFFFFFFFFu : 0u, sc.vis_cap * 2, s));
+        NR_CHECK(hipMemsetD32Async((hipDeviceptr_t)sc.vis, neutral ? 0xFFFFFFFFu : 0u, sc.vis_cap * 2, sa));
         sc.visNeutral = neutral;
     }
 
     auto grow_list = [&](size_t need) {
-        u32* lb[1] = {sc.flist};
-        const bool ok = grow_set(lb, &sc.flist_cap, std::max<size_t>(need, 1));
-        sc.flist = lb[0];
+        need = std::max<size_t>(need, 1);
+        if (F.flist_cap < need) quiesce();
+        u32* lb[1] = {F.flist};
+        const bool ok = grow_set(lb, &F.flist_cap, need);
+        F.flist = lb[0];
         return ok;
     };
     auto grow_items = [&](size_t need) {
-        uint4* ib[1] = {sc.fitems};
-        const bool ok = grow_set(ib, &sc.fitems_cap, std::max<size_t>(need, 1));
-        sc.fitems = ib[0];
+        need = std::max<size_t>(need, 1);
+        if (F.fitems_cap < need) quiesce();
+        uint4* ib[1] = {F.fitems};
+        const bool ok = grow_set(ib, &F.fitems_cap, need);
+        F.fitems = ib[0];
         return ok;
     };
-    u64* rb[1] = {sc.frect};
-    if (!grow_set(rb, &sc.frect_cap, (size_t)src.n)) return false;
-    sc.frect = rb[0];
+    if (F.frect_cap < (size_t)src.n) quiesce();
+    u64* rb[1] = {F.frect};
+    if (!grow_set(rb, &F.frect_cap, (size_t)src.n)) return false;
+    F.frect = rb[0];
     size_t cap;
     if (!exact) {
         const u64 est = std::max<u64>(std::max<u64>(sc.lastPairs + sc.lastPairs / 4, (u64)src.n * 2), 1u << 20);
         cap = (size_t)std::min<u64>(sc.capOverride ? sc.capOverride : est, 0xFFFFFFF0ull);
         if (!grow_list(cap)) return false;
-        if (!sc.capOverride) cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
+        if (!sc.capOverride) cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
         // work items: at most one per tile + one per full slice of the list
         if (!grow_items((size_t)ntiles + cap / SLICE + 2)) return false;
     } else {
         if (!grow_list(1) || !grow_items(1)) return false;
-        cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
+        cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
     }
 
     const bool ldsh = ntiles <= LDS_HIST_MAX;
@@ -837,57 +869,65 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     hipEvent_t e0, e1;
     u32 grid;
     for (int attempt = 0;; ++attempt) {
-        nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
-        if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.fcnt, ntiles, sc.frect);
-        else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, s, bp, sc.fcnt, ntiles, sc.frect);
+        nr_timing_begin_on(ctx, NRK_TRI_COUNT, &e0, &e1, sb);
+        if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, sb, bp, F.fcnt, ntiles, F.frect);
+        else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, sb, bp, F.fcnt, ntiles, F.frect);
         NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
+        nr_timing_end_on(ctx, NRK_TRI_COUNT, e0, e1, sb);
 
-        nr_timing_begin(ctx, NRK_TRI_SCAN, &e0, &e1);
-        hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, s, sc.fcnt, ntiles, fp.tiles_x, fp.nshards,
-                           fp.shard, sc.foff, sc.fitems, sc.fcur, sc.dplan, sc.d_hplan, (u32)cap,
-                           (u32)std::min<size_t>(sc.fitems_cap, 0xFFFFFFF0ull), ++sc.planSeq);
+        const u32 seq = ++sc.planSeq;
+        *seqOut = seq;
+        nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
+        hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.nshards,
+                           fp.shard, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
+                           (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq);
         NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_TRI_SCAN, e0, e1);
+        nr_timing_end_on(ctx, NRK_TRI_SCAN, e0, e1, sb);
 
         if (!exact) {
-            grid = (u32)std::min<u64>(sc.fitems_cap, 8192);   // grid-stride over the items
+            grid = (u32)std::min<u64>(F.fitems_cap, 8192);   // grid-stride over the items
             break;
         }
         // exact: read the totals back; if the list or the items did not fit,
         // grow both and bin again (the plan kernel re-zeroed the counters)
-        NR_CHECK(hipStreamSynchronize(s));
-        sc.lastPairs = sc.h_plan[0];
+        NR_CHECK(hipStreamSynchronize(sb));
+        sc.lastPairs = F.h_plan[0];
         sc.lastN = (u64)src.n;
-        grid = sc.h_plan[1];
-        if (sc.h_plan[3]) break;
-        if (attempt > 0 || !grow_list(sc.h_plan[0]) || !grow_items(sc.h_plan[1])) {
+        grid = F.h_plan[1];
+        if (F.h_plan[3]) break;
+        if (attempt > 0 || !grow_list(F.h_plan[0]) || !grow_items(F.h_plan[1])) {
             nr_set_error_msg("triangle binning: pair list allocation failed");
             return false;
         }
-        cap = std::min<size_t>(sc.flist_cap, 0xFFFFFFF0ull);
+        cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
     }
 
-    nr_timing_begin(ctx, NRK_TRI_EMIT, &e0, &e1);
-    if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.frect, sc.dplan);
-    else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, s, bp, sc.foff, sc.fcur, sc.flist, ntiles, sc.frect, sc.dplan);
+    nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
+    if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, sb, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, F.dplan);
+    else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, sb, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, F.dplan);
     NR_CHECK(hipGetLastError());
-    nr_timing_end(ctx, NRK_TRI_EMIT, e0, e1);
+    nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
+    if (sb != sa) {
+        NR_CHECK(hipEventRecord(F.evBin, sb));
+        NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
+    }
 
     if (grid > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, grid, s); else launch_vis_z<1, false>(fp, sc, grid, s); }
-        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, grid, s); else launch_vis_z<2, false>(fp, sc, grid, s); }
-        else { if (g) launch_vis_z<0, true>(fp, sc, grid, s); else launch_vis_z<0, false>(fp, sc, grid, s); }
+        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa); else launch_vis_z<1, false>(fp, sc, F, grid, sa); }
+        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa); else launch_vis_z<2, false>(fp, sc, F, grid, sa); }
+        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa); else launch_vis_z<0, false>(fp, sc, F, grid, sa); }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
     }
+    NR_CHECK(hipEventRecord(F.evVis, sa));
+    F.visRecorded = true;
     return true;
 }
 
 }  // namespace
 
-void draw_free(RenderContext* ctx, const TriSrc& src) {
+void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable) {
     FrameParams fp = frame_params(ctx, src);
     if (ctx->frameOutput && fp.pendColor) {
         const size_t n = (size_t)(ctx->width * ctx->height * fp.ipp);
@@ -900,9 +940,13 @@ void draw_free(RenderContext* ctx, const TriSrc& src) {
     bp.nshards = fp.nshards; bp.shard = fp.shard;
     // fragment counting reads a counter back anyway: run exact (synchronous)
     const bool exact = fp.fragCounter != nullptr;
-    if (!free_enqueue(ctx, src, fp, bp, exact)) return;
+    TriScratch& sc = ctx->tri;
+    const int si = sc.fnext;
+    sc.fnext ^= 1;
+    u32 seq = 0;
+    if (!free_enqueue(ctx, src, fp, bp, exact, si, immutable && !exact, &seq)) return;
     if (!exact) {
-        PendingBatch* pb = new PendingBatch{src, fp, bp};
+        PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq};
         ctx->pendingBatch = pb;
     }
     ctx->lastPath = 1;
@@ -919,15 +963,17 @@ void settle(RenderContext* ctx) {
     if (!pb) return;
     ctx->pendingBatch = nullptr;
     TriScratch& sc = ctx->tri;
+    TriScratch::FreeSet& F = sc.fset[pb->set];
     // wait for the batch's plan (usually long finished): it writes its
     // sequence number into pinned host memory after the totals -- polling it
     // avoids an event record per batch (each costs a multi-microsecond
     // bubble on the stream)
-    const u32 want = sc.planSeq;
-    for (u64 spin = 0; __atomic_load_n(&sc.h_plan[4], __ATOMIC_ACQUIRE) != want; ++spin) {
+    const u32 want = pb->seq;
+    for (u64 spin = 0; __atomic_load_n(&F.h_plan[4], __ATOMIC_ACQUIRE) != want; ++spin) {
         if ((spin & 1023) == 1023) {
-            const hipError_t q = hipStreamQuery(ctx->stream);
-            if (q != hipErrorNotReady && __atomic_load_n(&sc.h_plan[4], __ATOMIC_ACQUIRE) != want) {
+            const bool idle = hipStreamQuery(ctx->stream) != hipErrorNotReady &&
+                              hipStreamQuery(nr_bin_stream_for(ctx->device)) != hipErrorNotReady;
+            if (idle && __atomic_load_n(&F.h_plan[4], __ATOMIC_ACQUIRE) != want) {
                 nr_set_error_msg("triangle batch: plan result missing (stream idle or failed)");
                 delete pb;
                 return;
@@ -936,11 +982,13 @@ void settle(RenderContext* ctx) {
         }
     }
     sc.lastN = (u64)pb->src.n;
-    if (sc.h_plan[3]) {
-        sc.lastPairs = sc.h_plan[0];
-    } else {
-        sc.lastPairs = sc.h_plan[0];
-        free_enqueue(ctx, pb->src, pb->fp, pb->bp, true);   // context flags were applied at the first launch
+    sc.lastPairs = F.h_plan[0];
+    if (!F.h_plan[3]) {
+        // overflow: the batch's later kernels did nothing; re-run it exactly
+        // on the main stream, after everything queued so far
+        NR_CHECK(hipEventSynchronize(F.evVis));
+        u32 seq = 0;
+        free_enqueue(ctx, pb->src, pb->fp, pb->bp, true, pb->set, false, &seq);   // context flags applied at the first launch
     }
     delete pb;
 }
