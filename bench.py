@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--extra", action="store_true", help="also time c2/c5 and report them under 'extra'")
     ap.add_argument("--no-kernel-timing", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
+    ap.add_argument("--emulate-shards", type=int, default=0,
+                    help="experiment: render shard 0 of N on this one GPU (no gather) to time one rank's share")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,6 +151,8 @@ def main():
         from libnativecpurenderer_amd import sharding
         ctx.set_shard(world, rank)
         comm = sharding.make_comm(dist, world, rank)
+    elif args.emulate_shards > 1:
+        ctx.set_shard(args.emulate_shards, 0)
 
     def frame():
         ctx.set_color(0, 0, 0, 0)
@@ -195,7 +199,8 @@ def main():
             kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
     path = ctx.last_raster_path()
     from libnativecpurenderer_amd import sharding
-    frac = len(sharding.owned_rows(H, world, rank)) / H
+    nsh = args.emulate_shards if (world == 1 and args.emulate_shards > 1) else world
+    frac = len(sharding.owned_rows(H, nsh, rank)) / H
     kb = kernel_bytes(cfg, n_tri, path, frac)
     dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
@@ -244,6 +249,7 @@ def main():
         "config": {"workload": cfg["desc"], "width": W, "height": H, "triangles": n_tri,
                    "fragments_per_frame": int(frags), "frame_pixels": W * H,
                    "parallelism": (f"tile-row shards x{world} + RCCL u8 frame gather" if world > 1
+                                   else f"EMULATED shard 0 of {nsh} on one GPU (no gather)" if nsh > 1
                                    else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBPS, "unit": "GB/s",

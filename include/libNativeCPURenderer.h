@@ -117,6 +117,8 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root);  /* u8 frame (cp
 void GetFrameU8(RenderContext* ctx, iu8* out);
 void* GetFrameU8DevicePtr(RenderContext* ctx);
 bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root); /* f64 + depth bands to root */
+bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root); /* tests: GatherFrameU8's packed assembly of n
+                                                                    shards of one process, device copies for RCCL */
 
 /* ---- NEW: deferred command list ---------------------------
  * Replaces the reference's recording proxy MultiThreadedVideoRenderContext-

@@ -99,6 +99,7 @@ DEVICE_ABI = {
     "GetFrameU8": (None, (P, P)),
     "GetFrameU8DevicePtr": (P, (P,)),
     "GatherFramebuffer": (B, (P, P, L)),
+    "GatherFrameU8Local": (B, (P, L, L)),
     "EnableKernelTiming": (None, (P, B)),
     "GetKernelTiming": (B, (P, ctypes.c_char_p, P, P)),
     "ResetKernelTiming": (None, (P,)),

@@ -108,6 +108,7 @@ struct RenderContext {
     // multi-GPU: owned tile rows ty % nshards == shard (nr_dist.hip)
     int nshards = 1, shard = 0;
     iu8* frameU8 = nullptr; size_t frameU8cap = 0;   // assembled u8 frame (GatherFrameU8)
+    iu8* frameStage = nullptr; size_t frameStageCap = 0;   // packed bands of the gather
     bool frameOutput = false;   // set by GatherFrameU8: resolves also write the u8 frame
     bool frameU8Valid = false;  // frameU8 holds the u8 image of every owned pixel
     void* pendingBatch = nullptr;   // last visibility batch awaiting validation (nr_settle)

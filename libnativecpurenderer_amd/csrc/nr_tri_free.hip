@@ -29,6 +29,7 @@
 //                    it and resets those keys.
 #include "nr_tri.h"
 
+#include <cstdlib>
 #include <thread>
 
 namespace nrtri {
@@ -47,7 +48,14 @@ constexpr int VWG = NR_VWG;  // k_vis workgroup
 #ifndef NR_SLICE
 #define NR_SLICE 1024
 #endif
-constexpr u32 SLICE = NR_SLICE;   // triangles per work item
+constexpr u32 SLICE = NR_SLICE;   // longest work item (triangles)
+#ifndef NR_SLICE_MIN
+#define NR_SLICE_MIN 64
+#endif
+constexpr u32 SLICE_MIN = NR_SLICE_MIN;   // shortest slice of a split tile
+#ifndef NR_SLICE_TARGET
+#define NR_SLICE_TARGET 512
+#endif
 constexpr int TPT = 4;       // triangles per thread in the binning kernels
 constexpr int LDS_HIST_MAX = 16384;
 
@@ -105,8 +113,8 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
 // It also re-zeroes the tile counters for the next batch (after reading them)
 // and the emit cursors, and mirrors the totals into pinned host memory, so a
 // batch needs no memset and no copy command.
-__device__ __forceinline__ u32 tile_items(u32 c, bool owned) {
-    return owned ? (c > SLICE ? (c + SLICE - 1) / SLICE : 1u) : 0u;
+__device__ __forceinline__ u32 tile_items(u32 c, bool owned, u32 slice) {
+    return owned ? (c > slice ? (c + slice - 1) / slice : 1u) : 0u;
 }
 
 // Inclusive wave scan (64 lanes).
@@ -127,8 +135,8 @@ constexpr int PLAN_NB = 12;
 // laid out largest class first: k_vis workgroups take items in index order,
 // so the long ones start first and the short ones fill the tail (a longest-
 // first schedule).  Results do not depend on the order (order-free raster).
-__device__ __forceinline__ int size_class(u32 c) {
-    if (c > SLICE) return PLAN_NB - 1;
+__device__ __forceinline__ int size_class(u32 c, u32 slice) {
+    if (c > slice) return PLAN_NB - 1;
     if (c == 0) return 0;
     const int l = 31 - __clz(c);
     return 1 + (l < PLAN_NB - 3 ? l : PLAN_NB - 3);
@@ -139,29 +147,43 @@ __device__ __forceinline__ int size_class(u32 c) {
 __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int nshards,
                                                       int shard, u32* __restrict__ off, uint4* __restrict__ items,
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
-                                                      u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq) {
+                                                      u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
+                                                      u32 slice_target) {
     __shared__ u32 sh[3][PLAN_W];
     __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid < PLAN_NB) bcnt[tid] = 0;
+    // pass 0: the pair total sets the slice length, the smallest power of two
+    // in [SLICE_MIN, SLICE] giving at most ~slice_target items of work
+    // (short lists are sliced finer so that a sharded frame, whose dense tiles
+    // are few, still fills the chip)
+    u32 a = 0;
+    for (int i = tid; i < ntiles; i += PLAN_T) a += cnt[i];
+    a = wave_scan(a, lane);
+    if (lane == 63) sh[0][w] = a;
     __syncthreads();
-    // pass 1: totals (the capacity check needs them before any item is
+    u32 ta = 0;
+#pragma unroll
+    for (int k = 0; k < PLAN_W; ++k) ta += sh[0][k];
+    u32 slice = SLICE_MIN;
+    while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
+    __syncthreads();
+    // pass 1: items (the capacity check needs the totals before any item is
     // written) and the number of items per size class
-    u32 a = 0, b = 0, m = 0;
+    u32 b = 0, m = 0;
     for (int i = tid; i < ntiles; i += PLAN_T) {
         const u32 c = cnt[i];
-        const u32 ni = tile_items(c, owned_row(i / tiles_x, nshards, shard));
-        a += c;
+        const u32 ni = tile_items(c, owned_row(i / tiles_x, nshards, shard), slice);
         b += ni;
-        m += c > SLICE ? 1u : 0u;
-        if (ni) atomicAdd(&bcnt[size_class(c)], ni);
+        m += c > slice ? 1u : 0u;
+        if (ni) atomicAdd(&bcnt[size_class(c, slice)], ni);
     }
-    a = wave_scan(a, lane); b = wave_scan(b, lane); m = wave_scan(m, lane);
-    if (lane == 63) { sh[0][w] = a; sh[1][w] = b; sh[2][w] = m; }
+    b = wave_scan(b, lane); m = wave_scan(m, lane);
+    if (lane == 63) { sh[1][w] = b; sh[2][w] = m; }
     __syncthreads();
-    u32 ta = 0, tb = 0, tm = 0;
+    u32 tb = 0, tm = 0;
 #pragma unroll
-    for (int k = 0; k < PLAN_W; ++k) { ta += sh[0][k]; tb += sh[1][k]; tm += sh[2][k]; }
+    for (int k = 0; k < PLAN_W; ++k) { tb += sh[1][k]; tm += sh[2][k]; }
     const bool fits = ta <= cap && tb <= icap;
     if (tid == 0) {   // item ranges of the classes, largest class first
         u32 base = 0;
@@ -175,7 +197,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         u32 c = 0, ni = 0;
         if (i < ntiles) {
             c = cnt[i];
-            ni = tile_items(c, owned_row(i / tiles_x, nshards, shard));
+            ni = tile_items(c, owned_row(i / tiles_x, nshards, shard), slice);
         }
         const u32 ia = wave_scan(c, lane);
         if (lane == 63) sh[0][w] = ia;
@@ -190,10 +212,10 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         if (i < ntiles) {
             off[i] = ea;
             if (fits && ni) {
-                const u32 eb = atomicAdd(&bcur[size_class(c)], ni);
+                const u32 eb = atomicAdd(&bcur[size_class(c, slice)], ni);
                 for (u32 k = 0; k < ni; ++k) {
-                    const u32 ls = ea + k * SLICE;
-                    items[eb + k] = make_uint4((u32)i, ls, min(ls + SLICE, ea + c), ni);
+                    const u32 ls = ea + k * slice;
+                    items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + c), ni);
                 }
             }
             cnt[i] = 0;
@@ -582,7 +604,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         // blocks of rows sized to the widest span).  A short slice is cut into NW chunks so that every
         // wave gets a share.
         const u32 ns = le - ls;
-        const u32 cs = (!COOP || ns >= 64u * NW) ? 64u : (ns + NW - 1) / NW;
+        const u32 cs = ns >= 64u * NW ? 64u : (ns + NW - 1) / NW;
         const u32 nch = (ns + cs - 1) / cs;
         u32 pt = 0;
         f64 pxy[6], pz[3] = {0, 0, 0};
@@ -768,6 +790,17 @@ struct PendingBatch {
     u32 seq;
 };
 
+// Items the plan kernel aims for when it picks the slice length
+// (NR_SLICE_TARGET; the environment variable of the same name overrides it).
+static u32 slice_target() {
+    static const u32 v = [] {
+        const char* e = getenv("NR_SLICE_TARGET");
+        const long x = e ? atol(e) : 0;
+        return x > 0 ? (u32)x : (u32)NR_SLICE_TARGET;
+    }();
+    return v;
+}
+
 static hipEvent_t sync_event() {
     hipEvent_t e;
     NR_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
@@ -857,7 +890,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         if (!grow_list(cap)) return false;
         if (!sc.capOverride) cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
         // work items: at most one per tile + one per full slice of the list
-        if (!grow_items((size_t)ntiles + cap / SLICE + 2)) return false;
+        if (!grow_items((size_t)ntiles + cap / SLICE_MIN + 2)) return false;
     } else {
         if (!grow_list(1) || !grow_items(1)) return false;
         cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
@@ -880,7 +913,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
         hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.nshards,
                            fp.shard, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
-                           (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq);
+                           (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_SCAN, e0, e1, sb);
 

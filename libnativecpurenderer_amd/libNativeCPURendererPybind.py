@@ -318,6 +318,15 @@ class RenderContext:
         lib.GetFrameU8(self._ptr, out.ctypes.data_as(ctypes.c_void_p))
         return out
 
+    @staticmethod
+    def gather_frame_u8_local(ctxs: typing.Sequence["RenderContext"], root: int = 0):
+        """Testing: GatherFrameU8's packed band assembly for shards 0..n-1 of
+        one process (ctxs[p] renders shard p of n), with device copies in
+        place of the RCCL send/recv; the frame is assembled on ctxs[root]."""
+        arr = (ctypes.c_void_p * len(ctxs))(*[c._ptr for c in ctxs])
+        if not lib.GatherFrameU8Local(arr, len(ctxs), root):
+            raise RuntimeError("GatherFrameU8Local failed: " + _lib.last_error())
+
     def gather_framebuffer(self, comm: "Comm", root: int = 0):
         """f64 framebuffer (+ depth) bands of every rank assembled on `root`."""
         if not lib.GatherFramebuffer(self._ptr, comm._ptr, root):

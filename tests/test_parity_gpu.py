@@ -263,6 +263,41 @@ def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, opaque):
     assert np.array_equal(fullu8, ctx.get_buffer_as_uint8_numpy())
 
 
+@pytest.mark.parametrize("nshards,root,W,H,alpha", [(2, 0, 333, 250, False), (3, 1, 333, 250, True),
+                                                     (8, 0, 256, 300, False), (8, 5, 100, 40, False)])
+def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha):
+    """GatherFrameU8's assembly (each rank's bands packed into one message,
+    one unpack on the root), run for n shards on one GPU with device copies in
+    place of RCCL: the root's u8 frame equals the unsharded frame byte for
+    byte (odd widths take the byte-wise copy, multiples of 16 the vector one)."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    xy, z, c = scenes.triangle_soup(2000, W, H, 18, seed=43, gouraud=True)
+
+    def render(n, r):
+        ctx = gpu.context(W, H, alpha)
+        ctx.set_shard(n, r)
+        ctx.set_color(0.2, 0.1, 0.3, 1.0)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.draw_triangles(xy, c, z=z)
+        return ctx
+
+    ref = render(1, 0)
+    ref.gather_frame_u8()
+    want = ref.get_frame_u8()
+    ctxs = [render(nshards, r) for r in range(nshards)]
+    R.RenderContext.gather_frame_u8_local(ctxs, root)
+    got = ctxs[root].get_frame_u8()
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    # a second frame through the same staging buffers
+    for ctx in ctxs:
+        ctx.fill_color(0.5, 0.25, 0.75, 0.5)
+    ref.fill_color(0.5, 0.25, 0.75, 0.5)
+    ref.gather_frame_u8()
+    R.RenderContext.gather_frame_u8_local(ctxs, root)
+    assert np.array_equal(ctxs[root].get_frame_u8(), ref.get_frame_u8())
+
+
 def test_single_rank_comm_gather(gpu):
     """The RCCL path with a one-rank communicator (a no-op assembly)."""
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
