@@ -81,7 +81,7 @@ enum {
 };
 
 template <bool GOURAUD, bool DEPTH, bool COUNT>
-__global__ __launch_bounds__(WG) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
                                                     const u32* __restrict__ tstart, const u32* __restrict__ tend) {
     const int tile = blockIdx.x;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
@@ -181,12 +181,31 @@ __global__ __launch_bounds__(WG) void k_tile_raster(const FrameParams fp, const 
             }
         }
         __syncthreads();
-        // ---- (c) in-order raster of the chunk; each wave owns 4 rows
+        // ---- (c) in-order raster of the chunk; each wave owns 4 rows.
+        // Every product of the per-pixel expressions that is constant along
+        // a column (dx * e2y, dx * e1y), along a row (e2x * dy, e1x * dy) or
+        // over the triangle (flat: src * colourTransform, src * a, 1 - a) is
+        // formed once there: the same rounded values in the same expression
+        // trees, so the result is bit-identical to the per-pixel form.
+        const f64 X = (f64)(x0 + lane);
         for (int k = 0; k < cnt; ++k) {
             if (!NE[k][wave]) continue;
             const f64 sx0 = S[S_X0][k], sy0 = S[S_Y0][k];
             const f64 e1x = S[S_E1X][k], e1y = S[S_E1Y][k], e2x = S[S_E2X][k], e2y = S[S_E2Y][k];
             const f64 inv = S[S_INV][k];
+            f64 pa = 0, pb = 0;   // dx * e2y, dx * e1y of this lane's column
+            if (DEPTH || GOURAUD) {
+                const f64 dx = X - sx0;
+                pa = dx * e2y;
+                pb = dx * e1y;
+            }
+            f64 fR = 0, fG = 0, fB = 0, fA = 1, om = 0, RA = 0, GA = 0, BA = 0;
+            if (!GOURAUD) {   // ApplyPixel's per-triangle terms (cpp:529-535)
+                fR = S[S_C0 + 0][k] * ct0; fG = S[S_C0 + 1][k] * ct1;
+                fB = S[S_C0 + 2][k] * ct2; fA = S[S_C0 + 3][k] * ct3;
+                om = 1 - fA;
+                RA = fR * fA; GA = fG * fA; BA = fB * fA;
+            }
 #pragma unroll
             for (int r = 0; r < RPW; ++r) {
                 const int row = wave * RPW + r;
@@ -194,9 +213,9 @@ __global__ __launch_bounds__(WG) void k_tile_raster(const FrameParams fp, const 
                 if (lane < xs || lane >= xe) continue;
                 f64 w1 = 0, w2 = 0;
                 if (DEPTH || GOURAUD) {
-                    const f64 dx = (f64)(x0 + lane) - sx0, dy = (f64)(y0 + row) - sy0;
-                    w1 = (dx * e2y - e2x * dy) * inv;
-                    w2 = (e1x * dy - dx * e1y) * inv;
+                    const f64 dy = (f64)(y0 + row) - sy0;
+                    w1 = (pa - e2x * dy) * inv;
+                    w2 = (e1x * dy - pb) * inv;
                 }
                 u32 zq = 0;
                 if (DEPTH) {
@@ -204,23 +223,27 @@ __global__ __launch_bounds__(WG) void k_tile_raster(const FrameParams fp, const 
                     zq = nr_quantize_depth(zz);
                     if (!(zq < cz[r])) continue;
                 }
-                f64 R, G, B, A;
                 if (GOURAUD) {
-                    R = S[S_C0 + 0][k] + S[S_D1 + 0][k] * w1 + S[S_D2 + 0][k] * w2;
-                    G = S[S_C0 + 1][k] + S[S_D1 + 1][k] * w1 + S[S_D2 + 1][k] * w2;
-                    B = S[S_C0 + 2][k] + S[S_D1 + 2][k] * w1 + S[S_D2 + 2][k] * w2;
-                    A = S[S_C0 + 3][k] + S[S_D1 + 3][k] * w1 + S[S_D2 + 3][k] * w2;
+                    f64 R = S[S_C0 + 0][k] + S[S_D1 + 0][k] * w1 + S[S_D2 + 0][k] * w2;
+                    f64 G = S[S_C0 + 1][k] + S[S_D1 + 1][k] * w1 + S[S_D2 + 1][k] * w2;
+                    f64 B = S[S_C0 + 2][k] + S[S_D1 + 2][k] * w1 + S[S_D2 + 2][k] * w2;
+                    f64 A = S[S_C0 + 3][k] + S[S_D1 + 3][k] * w1 + S[S_D2 + 3][k] * w2;
+                    // ApplyPixel (cpp:529-547) on the register-resident pixel
+                    R *= ct0; G *= ct1; B *= ct2; A *= ct3;
+                    if (A != 1) {
+                        R = cr[r] * (1 - A) + R * A;
+                        G = cg[r] * (1 - A) + G * A;
+                        B = cb[r] * (1 - A) + B * A;
+                    }
+                    cr[r] = R; cg[r] = G; cb[r] = B; ca[r] = A;
+                } else if (fA != 1) {
+                    cr[r] = cr[r] * om + RA;
+                    cg[r] = cg[r] * om + GA;
+                    cb[r] = cb[r] * om + BA;
+                    ca[r] = fA;
                 } else {
-                    R = S[S_C0 + 0][k]; G = S[S_C0 + 1][k]; B = S[S_C0 + 2][k]; A = S[S_C0 + 3][k];
+                    cr[r] = fR; cg[r] = fG; cb[r] = fB; ca[r] = fA;
                 }
-                // ApplyPixel (cpp:529-547) on the register-resident pixel
-                R *= ct0; G *= ct1; B *= ct2; A *= ct3;
-                if (A != 1) {
-                    R = cr[r] * (1 - A) + R * A;
-                    G = cg[r] * (1 - A) + G * A;
-                    B = cb[r] * (1 - A) + B * A;
-                }
-                cr[r] = R; cg[r] = G; cb[r] = B; ca[r] = A;
                 if (DEPTH && fp.depthWrite) cz[r] = zq;
             }
         }
