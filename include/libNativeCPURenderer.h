@@ -54,6 +54,14 @@ i64 GetTextureWidth(Texture* tex);                                       /* h:12
 i64 GetTextureHeight(Texture* tex);                                      /* h:121 */
 bool GetTextureEnableAlpha(Texture* tex);                                /* h:122 */
 
+/* ---- texture preparation: procedural hit-effect shader (cpp:1318-1440) */
+Texture* CreateMilthmHitEffectTexture(Texture* mask, f64 seed, f64 t, f64 r, f64 g, f64 b); /* h:151; NULL
+                                                                   when the mask has no alpha (cpp:1418) */
+void GetMilthmHitEffectPixel(f64 seed, f64 t, f64 x, f64 y, f64* a);     /* h:150 (inline there: not exported) */
+bool CreateMilthmHitEffectTextures(Texture* mask, f64 seed, const f64* ts, i64 n, f64 r, f64 g, f64 b,
+                                   Texture** out);  /* NEW: n thresholds ts[k] -> out[k], one launch
+                                                       (Helpers.create_milthm_hit_effect_textures, Pybind:34-48) */
+
 /* ---- transform / colour-transform state, host side (cpp:386-492, 623-641) */
 void SetTransform(RenderContext* ctx, f64 a, f64 b, f64 c, f64 d, f64 e, f64 f);   /* h:100 */
 void ApplyTransform(RenderContext* ctx, f64 a, f64 b, f64 c, f64 d, f64 e, f64 f); /* h:101 */

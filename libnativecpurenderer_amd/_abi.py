@@ -57,6 +57,8 @@ REFERENCE_ABI = {
     "GetTextureHeight": (L, (P,)),
     "GetTextureEnableAlpha": (B, (P,)),
     "GetVersion": (L, ()),
+    "CreateMilthmHitEffectTexture": (P, (P, D, D, D, D, D)),
+    "GetMilthmHitEffectPixel": (None, (D, D, D, D, P)),
 }
 
 # triangles / depth (also exported by the oracle)
@@ -100,6 +102,7 @@ DEVICE_ABI = {
     "GetFrameU8DevicePtr": (P, (P,)),
     "GatherFramebuffer": (B, (P, P, L)),
     "GatherFrameU8Local": (B, (P, L, L)),
+    "CreateMilthmHitEffectTextures": (B, (P, D, P, L, D, D, D, P)),
     "EnableKernelTiming": (None, (P, B)),
     "GetKernelTiming": (B, (P, ctypes.c_char_p, P, P)),
     "ResetKernelTiming": (None, (P,)),
@@ -112,7 +115,8 @@ DEVICE_ABI = {
 }
 
 HIP_LIBRARY_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **DEVICE_ABI}
-ORACLE_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, "OracleLastFragmentCount": (L, ())}
+ORACLE_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, "OracleLastFragmentCount": (L, ()),
+              "OracleGetTextureBuffer": (None, (P, P))}
 
 
 def bind(lib: ctypes.CDLL, table: dict) -> ctypes.CDLL:

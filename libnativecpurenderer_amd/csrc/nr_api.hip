@@ -786,3 +786,5 @@ void ResetKernelTiming(RenderContext* ctx) {
 }
 
 }  // extern "C"
+
+Texture* nr_new_texture(i64 w, i64 h, bool alpha) { return new_texture(w, h, alpha); }

@@ -139,6 +139,7 @@ struct TriangleBuffer {
 };
 
 // host helpers shared across translation units
+Texture* nr_new_texture(i64 w, i64 h, bool alpha);   // device texels, current device
 hipStream_t nr_stream_for(int device);
 hipStream_t nr_bin_stream_for(int device);        // second stream: triangle binning overlapped with the raster
 void nr_timing_begin_on(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b, hipStream_t s);

@@ -22,6 +22,7 @@ the milthm hit-effect shader and WapperedBytes helpers.
 from __future__ import annotations
 
 import ctypes
+import random
 import math
 import typing
 
@@ -56,8 +57,19 @@ class Helpers:
         raise NotImplementedError("WapperedBytes belong to the audio back-end (out of scope)")
 
     @staticmethod
-    def create_milthm_hit_effect_textures(mask: "Texture", n: int):
-        raise NotImplementedError("the procedural hit-effect shader is out of scope (SURVEY §8f-3)")
+    def create_milthm_hit_effect_textures(mask: "Texture", n: int, seed: typing.Optional[float] = None):
+        """n hit-effect textures of `mask` at thresholds i / (n - 1) with one
+        random seed and the colour #9690fd (Pybind:34-48), made by one launch
+        (CreateMilthmHitEffectTextures).  `seed` (new, keyword) fixes the seed;
+        n == 1 raises ZeroDivisionError like the reference."""
+        if seed is None:
+            seed = random.random()
+        ts = [i / (n - 1) for i in range(n)]
+        arr = (ctypes.c_double * max(n, 1))(*ts)
+        out = (ctypes.c_void_p * max(n, 1))()
+        if not lib.CreateMilthmHitEffectTextures(mask._ptr, seed, arr, n, 0x96 / 0xff, 0x90 / 0xff, 0xfd / 0xff, out):
+            raise RuntimeError("CreateMilthmHitEffectTextures failed (mask without alpha?) " + _lib.last_error())
+        return [PtrCreatedTexture(out[i]) for i in range(n)]
 
 
 class RenderContext:

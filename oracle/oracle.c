@@ -533,6 +533,67 @@ i64 GetTextureWidth(Texture *t) { return t->width; }
 i64 GetTextureHeight(Texture *t) { return t->height; }
 bool GetTextureEnableAlpha(Texture *t) { return t->enableAlpha; }
 
+/* ---- texture preparation: the procedural hit-effect shader, cpp:1318-1440 ----
+ * ShaderUtils in f64, left to right, no FMA.  `abs(atan2(...))` (cpp:1388) is
+ * the double overload in the reference build: its header includes FFmpeg's,
+ * libavutil/common.h includes <math.h>, and libstdc++'s <math.h> brings
+ * std::abs(double) into the global namespace (so fabs here). */
+static f64 sh_fract(f64 x) { return x - floor(x); }                                    /* cpp:1333-1335 */
+static f64 sh_rand(f64 nx, f64 ny) { return sh_fract(sin(nx * 12.9898 + ny * 78.233) * 43758.5453); } /* :1341 */
+static f64 sh_mix(f64 a, f64 b, f64 t) { return a + (b - a) * t; }                    /* cpp:1357-1359 */
+static f64 sh_noise(f64 px, f64 py) {                                                   /* cpp:1370-1381 */
+    f64 ipx = floor(px), ipy = floor(py);
+    f64 ux = sh_fract(px), uy = sh_fract(py);
+    f64 a = sh_rand(ipx, ipy);
+    f64 b = sh_rand(ipx + 1.0, ipy + 0.0);
+    f64 c = sh_rand(ipx + 0.0, ipy + 1.0);
+    f64 d = sh_rand(ipx + 1.0, ipy + 1.0);
+    f64 sx = ux * ux * (3.0 - 2.0 * ux), sy = uy * uy * (3.0 - 2.0 * uy);
+    return sh_mix(sh_mix(a, b, sx), sh_mix(c, d, sx), sy);
+}
+static f64 sh_circular_noise(f64 uvx, f64 uvy, f64 density, f64 seed) {                /* cpp:1384-1401 */
+    f64 cx = uvx - 0.5, cy = uvy - 0.5;
+    f64 radius = sqrt(cx * cx + cy * cy) * density;
+    f64 angle = fabs(atan2(cy, cx));
+    if (uvy > 0.5) angle += sin(angle) * 2.0;
+    f64 px = radius + seed * 100.0, py = angle + seed * 100.0;
+    f64 n = 0.0;
+    n += sh_noise(px, py) * 0.7;
+    n += sh_noise(px * 2.0, py * 2.0) * 0.3;
+    n += sh_noise(px * 4.0, py * 4.0) * 0.1;
+    return n;
+}
+
+/* cpp:1405-1410 (inline in the reference) */
+void GetMilthmHitEffectPixel(f64 seed, f64 t, f64 x, f64 y, f64 *a) {
+    f64 n = sh_circular_noise(x, y, 50.0, seed);
+    *a = (n < t) ? 0.0 : 1.0;
+}
+
+/* cpp:1416-1438: texel (i, j) at (i * h + j) * 4, the mask read at the same
+ * index (GetPixelChannel, cpp:1412-1414) — column-major; NULL without alpha */
+Texture *CreateMilthmHitEffectTexture(Texture *mask, f64 seed, f64 t, f64 r, f64 g, f64 b) {
+    if (!mask->enableAlpha) return NULL;
+    Texture *tex = (Texture *)calloc(1, sizeof(Texture));
+    tex->width = mask->width; tex->height = mask->height; tex->enableAlpha = true;
+    tex->buffer = (f64 *)malloc((size_t)(mask->width * mask->height * 4 > 0 ? mask->width * mask->height * 4 : 1)
+                                * sizeof(f64));
+    for (i64 i = 0; i < mask->width; ++i)
+        for (i64 j = 0; j < mask->height; ++j) {
+            f64 a;
+            GetMilthmHitEffectPixel(seed, t, (f64)i / mask->width, (f64)j / mask->height, &a);
+            f64 mask_a = mask->buffer[i * mask->height * 4 + j * 4 + 3];
+            f64 *o = tex->buffer + i * mask->height * 4 + j * 4;
+            o[0] = r; o[1] = g; o[2] = b; o[3] = a * mask_a;
+        }
+    return tex;
+}
+
+/* Oracle-only: a texture's texels (tests compare them with the GPU's). */
+void OracleGetTextureBuffer(Texture *t, f64 *out) {
+    memcpy(out, t->buffer, (size_t)(t->width * t->height * (t->enableAlpha ? 4 : 3)) * sizeof(f64));
+}
+
 /* h:9 / cpp GetVersion */
 i64 GetVersion(void) { return 1; }
 

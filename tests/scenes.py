@@ -627,3 +627,25 @@ def first_mismatch(a, b):
         return None
     i = tuple(idx[0])
     return f"{len(idx)} mismatches, first at {i}: {a[i]!r} vs {b[i]!r}"
+
+
+# ---------------------------------------------------------------------------
+# hit-effect texture (cpp:1318-1440) on both sides
+# ---------------------------------------------------------------------------
+def hit_mask(w, h, seed=7):
+    """Seeded RGBA u8 mask (non-square shapes exercise the column-major
+    indexing of cpp:1413-1432)."""
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 256, size=(h, w, 4), dtype=np.uint8)
+
+
+def oracle_hit_effect(mask_u8, seed, t, rgb=(0x96 / 0xff, 0x90 / 0xff, 0xfd / 0xff)):
+    lib = _OracleLib.get()
+    h, w, _ = mask_u8.shape
+    m = lib.CreateTextureUInt8(w, h, True, _vp(np.ascontiguousarray(mask_u8)))
+    tex = lib.CreateMilthmHitEffectTexture(m, seed, t, *rgb)
+    out = np.empty((h, w, 4), dtype=np.float64)
+    lib.OracleGetTextureBuffer(tex, _vp(out))
+    lib.DestroyTexture(tex)
+    lib.DestroyTexture(m)
+    return out

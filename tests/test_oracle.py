@@ -344,3 +344,56 @@ def test_sphere_mesh_shape():
     xy, z, c = scenes.sphere_mesh(64, 48, 10, 20)
     assert xy.shape == (400, 6) and z.shape == (400, 3) and c.shape == (400, 12)
     assert np.all((z > 0) & (z < 1))
+
+
+def _py_hit_pixel(seed, t, x, y):
+    """Independent restatement of cpp:1318-1410 (Python floats are the same
+    IEEE doubles and libm): GetMilthmHitEffectPixel."""
+    fract = lambda v: v - math.floor(v)
+    rand = lambda nx, ny: fract(math.sin(nx * 12.9898 + ny * 78.233) * 43758.5453)
+    mix = lambda a, b, k: a + (b - a) * k
+
+    def noise(px, py):
+        ix, iy = math.floor(px), math.floor(py)
+        ux, uy = fract(px), fract(py)
+        a, b = rand(ix, iy), rand(ix + 1.0, iy + 0.0)
+        c, d = rand(ix + 0.0, iy + 1.0), rand(ix + 1.0, iy + 1.0)
+        sx, sy = ux * ux * (3.0 - 2.0 * ux), uy * uy * (3.0 - 2.0 * uy)
+        return mix(mix(a, b, sx), mix(c, d, sx), sy)
+
+    cx, cy = x - 0.5, y - 0.5
+    radius = math.sqrt(cx * cx + cy * cy) * 50.0
+    angle = abs(math.atan2(cy, cx))          # std::abs(double) in the reference build
+    if y > 0.5:
+        angle += math.sin(angle) * 2.0
+    px, py = radius + seed * 100.0, angle + seed * 100.0
+    n = 0.0
+    n += noise(px, py) * 0.7
+    n += noise(px * 2.0, py * 2.0) * 0.3
+    n += noise(px * 4.0, py * 4.0) * 0.1
+    return 0.0 if n < t else 1.0
+
+
+@pytest.mark.parametrize("w,h", [(9, 13), (16, 16)])
+def test_oracle_hit_effect_texture(w, h):
+    """CreateMilthmHitEffectTexture (cpp:1416-1438): colour constant, alpha =
+    pixel(i/w, j/h) * mask alpha, texel (i, j) stored at (i*h + j)*4 and the
+    mask read at that same index (column-major, cpp:1413-1432)."""
+    mask = scenes.hit_mask(w, h)
+    seed, t = 0.37, 0.45
+    out = scenes.oracle_hit_effect(mask, seed, t).reshape(-1)
+    flat_mask = (mask.astype(np.float64) / 255.0).reshape(-1)
+    for i in range(w):
+        for j in range(h):
+            q = (i * h + j) * 4
+            want = _py_hit_pixel(seed, t, i / w, j / h) * flat_mask[q + 3]
+            assert out[q + 3] == want, (i, j)
+            assert out[q] == 0x96 / 0xff and out[q + 1] == 0x90 / 0xff and out[q + 2] == 0xfd / 0xff
+    assert 0 < np.count_nonzero(out[3::4]) < w * h   # both sides of the threshold occur
+
+
+def test_oracle_hit_effect_needs_alpha():
+    lib = scenes._OracleLib.get()
+    rgb = np.zeros((4, 4, 3), dtype=np.uint8)
+    m = lib.CreateTextureUInt8(4, 4, False, rgb.ctypes.data_as(scenes.ctypes.c_void_p))
+    assert not lib.CreateMilthmHitEffectTexture(m, 0.1, 0.5, 1.0, 1.0, 1.0)   # NULL (cpp:1418)

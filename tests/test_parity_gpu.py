@@ -1,6 +1,7 @@
 """GPU parity: the HIP library (through its Pybind mirror) against the CPU
 oracle on the same seeded inputs, bit for bit (f64 framebuffer, u8 readback,
 u32 depth), at fixture sizes and at BASELINE.json's full sizes."""
+import ctypes
 import os
 
 import numpy as np
@@ -368,3 +369,43 @@ def test_rotate_uses_sincos_like_the_reference_build(gpu, oracle):
         g.rotate(float(a))
         o.rotate(float(a))
         assert g.get_transform() == o.get_transform(), a
+
+
+@pytest.mark.parametrize("shape", [(128, 128), (96, 40)])
+def test_hit_effect_textures_match_oracle(gpu, shape):
+    """Helpers.create_milthm_hit_effect_textures (Pybind:34-48, cpp:1318-1440):
+    n textures of one mask/seed from one launch equal the oracle's textures
+    texel for texel (binary alpha x mask alpha, column-major storage).  The
+    device sin/atan2 are within an ULP of glibc's; that can only flip a texel
+    whose noise lies within ~1e-11 of the threshold, which none of these do."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    w, h = shape
+    if shape == (128, 128):
+        mask = np.load(os.path.join(scenes.ROOT, "tests", "golden", "image_png_rgba.npy"))
+    else:
+        mask = scenes.hit_mask(w, h, seed=11)
+    n, seed = 6, 0.6180339887
+    texs = R.Helpers.create_milthm_hit_effect_textures(R.Texture.from_numpy(mask), n, seed=seed)
+    assert len(texs) == n
+    for i, tex in enumerate(texs):
+        assert (tex.width, tex.height, tex.enableAlpha) == (w, h, True)
+        got = tex.get_buffer_numpy().reshape(h, w, 4)
+        want = scenes.oracle_hit_effect(mask, seed, i / (n - 1))
+        assert scenes.bits_equal(got, want), scenes.first_mismatch(got, want)
+    # the single-texture entry point (h:151) and the inline pixel function (h:150)
+    mtex = R.Texture.from_numpy(mask)
+    single = R.PtrCreatedTexture(R.lib.CreateMilthmHitEffectTexture(mtex._ptr, seed, 0.3, 0.1, 0.2, 0.3))
+    want = scenes.oracle_hit_effect(mask, seed, 0.3, rgb=(0.1, 0.2, 0.3))
+    assert scenes.bits_equal(single.get_buffer_numpy().reshape(h, w, 4), want)
+    a = ctypes.c_double()
+    for x, y in [(0.1, 0.2), (0.75, 0.6), (0.5, 0.5)]:
+        R.lib.GetMilthmHitEffectPixel(seed, 0.4, x, y, ctypes.byref(a))
+        b = ctypes.c_double()
+        scenes._OracleLib.get().GetMilthmHitEffectPixel(seed, 0.4, x, y, ctypes.byref(b))
+        assert a.value == b.value
+
+
+def test_hit_effect_needs_alpha_mask(gpu):
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    tex = R.Texture.from_numpy(np.zeros((8, 8, 3), dtype=np.uint8))
+    assert not R.lib.CreateMilthmHitEffectTexture(tex._ptr, 0.1, 0.5, 1.0, 1.0, 1.0)
