@@ -350,10 +350,11 @@ void DestroyRenderContext(RenderContext* ctx) {
     }
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
+    nr_dist_release(ctx);
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
                     t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
-                    t.fdone,     t.vis,        ctx->frameU8, ctx->frameStage};
+                    t.fdone,     t.vis};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     for (auto& F : t.fset) {
@@ -726,6 +727,7 @@ void Flush(RenderContext* ctx) {
     NR_CHECK(hipSetDevice(ctx->device));
     nr_settle(ctx);
     NR_CHECK(hipStreamSynchronize(ctx->stream));
+    nr_dist_sync(ctx);
 }
 
 // Materialises deferred clears (tests use it to compare device state).

@@ -107,8 +107,16 @@ struct RenderContext {
     iu8* u8buf = nullptr; size_t u8cap = 0;   // GetBufferAsUInt8 staging
     // multi-GPU: owned tile rows ty % nshards == shard (nr_dist.hip)
     int nshards = 1, shard = 0;
-    iu8* frameU8 = nullptr; size_t frameU8cap = 0;   // assembled u8 frame (GatherFrameU8)
-    iu8* frameStage = nullptr; size_t frameStageCap = 0;   // packed bands of the gather
+    // u8 frame output (GatherFrameU8, nr_dist.hip): two frame buffers, the
+    // next frame renders into one while the other is assembled on the gather
+    // stream; frameU8 = frameBuf[frameCur]
+    iu8* frameU8 = nullptr; size_t frameU8cap = 0;
+    iu8* frameBuf[2] = {nullptr, nullptr};
+    int frameCur = 0, frameLast = -1;            // buffer being rendered / of the last GatherFrameU8
+    iu8* stageBuf[2] = {nullptr, nullptr}; size_t stageCap[2] = {0, 0};   // packed bands per buffer
+    hipStream_t commStream = nullptr;            // RCCL transfers + the root's unpack
+    hipEvent_t evFrameReady = nullptr, evGatherDone[2] = {nullptr, nullptr};
+    bool gatherPending[2] = {false, false};
     bool frameOutput = false;   // set by GatherFrameU8: resolves also write the u8 frame
     bool frameU8Valid = false;  // frameU8 holds the u8 image of every owned pixel
     void* pendingBatch = nullptr;   // last visibility batch awaiting validation (nr_settle)
@@ -140,6 +148,8 @@ struct TriangleBuffer {
 
 // host helpers shared across translation units
 Texture* nr_new_texture(i64 w, i64 h, bool alpha);   // device texels, current device
+void nr_dist_sync(RenderContext* ctx);      // wait for the frame-assembly stream
+void nr_dist_release(RenderContext* ctx);   // free the frame-output buffers
 hipStream_t nr_stream_for(int device);
 hipStream_t nr_bin_stream_for(int device);        // second stream: triangle binning overlapped with the raster
 void nr_timing_begin_on(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b, hipStream_t s);

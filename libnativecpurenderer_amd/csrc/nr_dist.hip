@@ -120,40 +120,68 @@ __global__ void k_band_copy(iu8* __restrict__ frame, iu8* __restrict__ stage, i6
     }
 }
 
-// Launches k_band_copy over every band (16-byte vectors when the row length
-// keeps every band 16-byte aligned).
-void band_copy(RenderContext* ctx, bool unpack, int nranks, int sel, i64 peerStride, i64 rowElems) {
+// Launches k_band_copy over every band on `st` (16-byte vectors when the row
+// length keeps every band 16-byte aligned).
+void band_copy(RenderContext* ctx, iu8* frame, iu8* stage, hipStream_t st, bool unpack, int nranks, int sel,
+               i64 peerStride, i64 rowElems) {
     const i64 bands = (ctx->height + BAND - 1) / BAND;
     const bool vec = rowElems % 16 == 0;
     const i64 per = BAND * rowElems / (vec ? 16 : 1);
     dim3 grid((unsigned)std::min<i64>((per + 255) / 256, 1024), (unsigned)bands);
     if (vec) {
-        if (unpack) hipLaunchKernelGGL((k_band_copy<uint4, true>), grid, dim3(256), 0, ctx->stream, ctx->frameU8,
-                                       ctx->frameStage, rowElems, ctx->height, nranks, sel, peerStride);
-        else hipLaunchKernelGGL((k_band_copy<uint4, false>), grid, dim3(256), 0, ctx->stream, ctx->frameU8,
-                                ctx->frameStage, rowElems, ctx->height, nranks, sel, peerStride);
+        if (unpack) hipLaunchKernelGGL((k_band_copy<uint4, true>), grid, dim3(256), 0, st, frame, stage, rowElems,
+                                       ctx->height, nranks, sel, peerStride);
+        else hipLaunchKernelGGL((k_band_copy<uint4, false>), grid, dim3(256), 0, st, frame, stage, rowElems,
+                                ctx->height, nranks, sel, peerStride);
     } else {
-        if (unpack) hipLaunchKernelGGL((k_band_copy<iu8, true>), grid, dim3(256), 0, ctx->stream, ctx->frameU8,
-                                       ctx->frameStage, rowElems, ctx->height, nranks, sel, peerStride);
-        else hipLaunchKernelGGL((k_band_copy<iu8, false>), grid, dim3(256), 0, ctx->stream, ctx->frameU8,
-                                ctx->frameStage, rowElems, ctx->height, nranks, sel, peerStride);
+        if (unpack) hipLaunchKernelGGL((k_band_copy<iu8, true>), grid, dim3(256), 0, st, frame, stage, rowElems,
+                                       ctx->height, nranks, sel, peerStride);
+        else hipLaunchKernelGGL((k_band_copy<iu8, false>), grid, dim3(256), 0, st, frame, stage, rowElems,
+                                ctx->height, nranks, sel, peerStride);
     }
     NR_CHECK(hipGetLastError());
 }
 
-// Staging of the packed gather: a non-root rank's own bands, or on the root
-// one slot of the largest share per rank.
-bool ensure_stage(RenderContext* ctx, size_t need) {
-    if (need <= ctx->frameStageCap) return true;
-    if (ctx->frameStage) NR_CHECK(hipFree(ctx->frameStage));
-    ctx->frameStage = nullptr;
-    ctx->frameStageCap = 0;
-    if (hipMalloc((void**)&ctx->frameStage, need) != hipSuccess) {
+// The context's gather stream and events (created on first use).  The
+// transfer of frame k runs there while the main stream renders frame k+1.
+void ensure_comm_stream(RenderContext* ctx) {
+    if (ctx->commStream) return;
+    NR_CHECK(hipStreamCreateWithFlags(&ctx->commStream, hipStreamNonBlocking));
+    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+    NR_CHECK(hipEventCreateWithFlags(&ctx->evFrameReady, fl));
+    for (auto& e : ctx->evGatherDone) NR_CHECK(hipEventCreateWithFlags(&e, fl));
+}
+
+// Staging buffer `x` of the packed gather (a non-root rank's own bands, or on
+// the root one slot of the largest share per rank).
+bool ensure_stage(RenderContext* ctx, int x, size_t need) {
+    if (need <= ctx->stageCap[x]) return true;
+    if (ctx->stageBuf[x]) {
+        if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
+        NR_CHECK(hipFree(ctx->stageBuf[x]));
+    }
+    ctx->stageBuf[x] = nullptr;
+    ctx->stageCap[x] = 0;
+    if (hipMalloc((void**)&ctx->stageBuf[x], need) != hipSuccess) {
         nr_set_error_msg("GatherFrameU8: hipMalloc of the staging buffer failed");
         return false;
     }
-    ctx->frameStageCap = need;
+    ctx->stageCap[x] = need;
     return true;
+}
+
+// After frame buffer x went out for assembly: the next frame renders into
+// the other buffer, once the transfer that last read it (two frames back) is
+// done -- the main stream waits for that on the device, the host never does.
+void rotate_frame(RenderContext* ctx, int x) {
+    NR_CHECK(hipEventRecord(ctx->evGatherDone[x], ctx->commStream));
+    ctx->gatherPending[x] = true;
+    ctx->frameLast = x;
+    const int y = 1 - x;
+    ctx->frameCur = y;
+    ctx->frameU8 = ctx->frameBuf[y];
+    ctx->frameU8Valid = false;
+    if (ctx->gatherPending[y]) NR_CHECK(hipStreamWaitEvent(ctx->stream, ctx->evGatherDone[y], 0));
 }
 
 // The u8 image of the owned bands (the first half of GatherFrameU8), converted
@@ -163,15 +191,24 @@ bool frame_u8_local(RenderContext* ctx) {
     const int ipp = ctx->enableAlpha ? 4 : 3;
     const i64 n = ctx->width * ctx->height * ipp;
     if (n <= 0) return true;
-    if ((size_t)n > ctx->frameU8cap) {
-        if (ctx->frameU8) NR_CHECK(hipFree(ctx->frameU8));
-        ctx->frameU8 = nullptr;
-        if (hipMalloc((void**)&ctx->frameU8, (size_t)n) != hipSuccess) {
-            nr_set_error_msg("GatherFrameU8: hipMalloc failed");
-            ctx->frameU8cap = 0;
-            return false;
+    if ((size_t)n > ctx->frameU8cap) {   // both frame buffers (the assembly alternates between them)
+        if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
+        for (int x = 0; x < 2; ++x) {
+            if (ctx->frameBuf[x]) NR_CHECK(hipFree(ctx->frameBuf[x]));
+            ctx->frameBuf[x] = nullptr;
+            ctx->gatherPending[x] = false;
         }
+        ctx->frameU8 = nullptr;
+        ctx->frameU8cap = 0;
+        ctx->frameLast = -1;
+        for (int x = 0; x < 2; ++x)
+            if (hipMalloc((void**)&ctx->frameBuf[x], (size_t)n) != hipSuccess) {
+                nr_set_error_msg("GatherFrameU8: hipMalloc failed");
+                return false;
+            }
         ctx->frameU8cap = (size_t)n;
+        ctx->frameU8 = ctx->frameBuf[ctx->frameCur];
+        ctx->frameU8Valid = false;
     }
     const i64 rowElems = ctx->width * ipp;
     const i64 bands = (ctx->height + BAND - 1) / BAND;
@@ -189,6 +226,7 @@ bool frame_u8_local(RenderContext* ctx) {
         nr_timing_end(ctx, NRK_OUTPUT, e0, e1);
     }
     ctx->frameU8Valid = true;
+    ctx->frameLast = ctx->frameCur;
     return true;
 }
 
@@ -262,39 +300,47 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
     }
     Rccl* r = rccl();
     if (!r) return false;
-    // one message per rank: every non-root rank packs its bands back to back
+    // One message per rank: every non-root rank packs its bands back to back
     // and sends them; the root receives each rank's pack into its own slot
     // and scatters all of them into place with one kernel (a send/recv per
-    // band would cost RCCL's per-operation latency ~H/32 times on the root)
-    const int n = comm->nranks, me = comm->rank;
+    // band would cost RCCL's per-operation latency ~H/32 times on the root).
+    // The transfer and the unpack run on the context's gather stream, so they
+    // overlap the next frame, which renders into the other frame buffer.
+    const int n = comm->nranks, me = comm->rank, x = ctx->frameCur;
     const i64 rowElems = ctx->width * (ctx->enableAlpha ? 4 : 3);
-    const i64 maxRows = owned_rows(ctx->height, n, 0);   // rank 0 owns the most bands
-    const i64 peerStride = maxRows * rowElems;
-    if (!ensure_stage(ctx, (size_t)(me == root ? n * peerStride : owned_rows(ctx->height, n, me) * rowElems)))
+    const i64 peerStride = owned_rows(ctx->height, n, 0) * rowElems;   // rank 0 owns the most bands
+    ensure_comm_stream(ctx);
+    if (!ensure_stage(ctx, x, (size_t)(me == root ? n * peerStride : owned_rows(ctx->height, n, me) * rowElems)))
         return false;
+    iu8* frame = ctx->frameBuf[x];
+    iu8* stage = ctx->stageBuf[x];
     hipEvent_t e0, e1;
     nr_timing_begin(ctx, NRK_GATHER, &e0, &e1);
-    if (me != root) band_copy(ctx, false, n, me, 0, rowElems);
+    if (me != root) band_copy(ctx, frame, stage, ctx->stream, false, n, me, 0, rowElems);
+    nr_timing_end(ctx, NRK_GATHER, e0, e1);
+    NR_CHECK(hipEventRecord(ctx->evFrameReady, ctx->stream));
+    NR_CHECK(hipStreamWaitEvent(ctx->commStream, ctx->evFrameReady, 0));
     bool ok = nccl_ok(r, r->GroupStart(), "ncclGroupStart");
     for (int p = 0; p < n && ok; ++p) {
         const size_t cnt = (size_t)(owned_rows(ctx->height, n, p) * rowElems);
         if (cnt == 0) continue;
         if (me == root && p != root)
-            ok = nccl_ok(r, r->Recv(ctx->frameStage + p * peerStride, cnt, ncclUint8, p, comm->comm, ctx->stream),
+            ok = nccl_ok(r, r->Recv(stage + p * peerStride, cnt, ncclUint8, p, comm->comm, ctx->commStream),
                          "ncclRecv");
         else if (me != root && p == me)
-            ok = nccl_ok(r, r->Send(ctx->frameStage, cnt, ncclUint8, (int)root, comm->comm, ctx->stream), "ncclSend");
+            ok = nccl_ok(r, r->Send(stage, cnt, ncclUint8, (int)root, comm->comm, ctx->commStream), "ncclSend");
     }
     ok = nccl_ok(r, r->GroupEnd(), "ncclGroupEnd") && ok;
-    if (ok && me == root) band_copy(ctx, true, n, (int)root, peerStride, rowElems);
-    nr_timing_end(ctx, NRK_GATHER, e0, e1);
+    if (ok && me == root) band_copy(ctx, frame, stage, ctx->commStream, true, n, (int)root, peerStride, rowElems);
+    rotate_frame(ctx, x);
     return ok;
 }
 
-// NEW (testing): the packed gather of GatherFrameU8 for n contexts of ONE
-// process (ctxs[p] renders shard p of n), with device copies in place of the
-// RCCL send/recv -- the same pack, slot layout and unpack kernels, so the
-// multi-GPU assembly is checked on a single GPU.
+// NEW (testing): GatherFrameU8 for n contexts of ONE process (ctxs[p] renders
+// shard p of n) with device copies in place of the RCCL send/recv: the same
+// packing, slot layout, unpack kernel, gather stream and frame-buffer
+// rotation, so the multi-GPU assembly (and its overlap with the next frame)
+// is checked on a single GPU.
 bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     if (n < 1 || root < 0 || root >= n) {
         nr_set_error_msg("GatherFrameU8Local: need 0 <= root < n");
@@ -304,8 +350,8 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     for (i64 p = 0; p < n; ++p) {
         RenderContext* c = ctxs[p];
         if (c->nshards != n || c->shard != p || c->width != rc->width || c->height != rc->height ||
-            c->enableAlpha != rc->enableAlpha) {
-            nr_set_error_msg("GatherFrameU8Local: ctxs[p] must be shard p of n, all of one size");
+            c->enableAlpha != rc->enableAlpha || c->device != rc->device) {
+            nr_set_error_msg("GatherFrameU8Local: ctxs[p] must be shard p of n, all of one size and device");
             return false;
         }
         NR_CHECK(hipSetDevice(c->device));
@@ -315,34 +361,54 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     const i64 rowElems = rc->width * (rc->enableAlpha ? 4 : 3);
     const i64 peerStride = owned_rows(rc->height, (int)n, 0) * rowElems;
     NR_CHECK(hipSetDevice(rc->device));
-    if (!ensure_stage(rc, (size_t)(n * peerStride))) return false;
+    ensure_comm_stream(rc);
+    const int xr = rc->frameCur;
+    if (!ensure_stage(rc, xr, (size_t)(n * peerStride))) return false;
+    for (i64 p = 0; p < n; ++p) {   // peers: pack on their stream, copy on the root's gather stream
+        if (p == root) continue;
+        RenderContext* c = ctxs[p];
+        ensure_comm_stream(c);
+        const int xp = c->frameCur;
+        const size_t cnt = (size_t)(owned_rows(c->height, (int)n, (int)p) * rowElems);
+        if (!ensure_stage(c, xp, cnt)) return false;
+        band_copy(c, c->frameBuf[xp], c->stageBuf[xp], c->stream, false, (int)n, (int)p, 0, rowElems);
+        NR_CHECK(hipEventRecord(c->evFrameReady, c->stream));
+        NR_CHECK(hipStreamWaitEvent(rc->commStream, c->evFrameReady, 0));
+        NR_CHECK(hipMemcpyAsync(rc->stageBuf[xr] + p * peerStride, c->stageBuf[xp], cnt, hipMemcpyDeviceToDevice,
+                                rc->commStream));
+    }
+    NR_CHECK(hipEventRecord(rc->evFrameReady, rc->stream));
+    NR_CHECK(hipStreamWaitEvent(rc->commStream, rc->evFrameReady, 0));
+    band_copy(rc, rc->frameBuf[xr], rc->stageBuf[xr], rc->commStream, true, (int)n, (int)root, peerStride, rowElems);
+    // the peers' stages were read on the root's gather stream: their own
+    // gather streams (whose events guard the buffers' reuse) wait for it
+    NR_CHECK(hipEventRecord(rc->evGatherDone[xr], rc->commStream));
     for (i64 p = 0; p < n; ++p) {
         if (p == root) continue;
         RenderContext* c = ctxs[p];
-        NR_CHECK(hipSetDevice(c->device));
-        const size_t cnt = (size_t)(owned_rows(c->height, (int)n, (int)p) * rowElems);
-        if (!ensure_stage(c, cnt)) return false;
-        band_copy(c, false, (int)n, (int)p, 0, rowElems);
-        NR_CHECK(hipStreamSynchronize(c->stream));
-        // on the root's (non-blocking) stream, so the unpack is ordered after it
-        NR_CHECK(hipMemcpyAsync(rc->frameStage + p * peerStride, c->frameStage, cnt, hipMemcpyDefault, rc->stream));
+        NR_CHECK(hipStreamWaitEvent(c->commStream, rc->evGatherDone[xr], 0));
+        rotate_frame(c, c->frameCur);
     }
-    NR_CHECK(hipSetDevice(rc->device));
-    band_copy(rc, true, (int)n, (int)root, peerStride, rowElems);
-    NR_CHECK(hipStreamSynchronize(rc->stream));
+    rotate_frame(rc, xr);
     return true;
 }
 
-// NEW: copy the assembled u8 frame to the host (valid on the root).
+// NEW: copy the frame of the last GatherFrameU8 to the host (the assembled
+// image on the root; a rank's own bands elsewhere).
 void GetFrameU8(RenderContext* ctx, iu8* out) {
     NR_CHECK(hipSetDevice(ctx->device));
-    if (!ctx->frameU8) return;
-    NR_CHECK(hipMemcpyAsync(out, ctx->frameU8, (size_t)(ctx->width * ctx->height * (ctx->enableAlpha ? 4 : 3)),
-                            hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->frameLast < 0 || !ctx->frameBuf[ctx->frameLast]) return;
+    if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
+    NR_CHECK(hipMemcpyAsync(out, ctx->frameBuf[ctx->frameLast],
+                            (size_t)(ctx->width * ctx->height * (ctx->enableAlpha ? 4 : 3)), hipMemcpyDeviceToHost,
+                            ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));
 }
 
-void* GetFrameU8DevicePtr(RenderContext* ctx) { return ctx->frameU8; }
+// NEW: device pointer of that frame (complete once Flush returns).
+void* GetFrameU8DevicePtr(RenderContext* ctx) {
+    return ctx->frameLast >= 0 ? ctx->frameBuf[ctx->frameLast] : ctx->frameU8;
+}
 
 // NEW: assemble the owned bands of the f64 framebuffer (and of the depth
 // buffer, when allocated) into the root's buffers — byte-exact N-GPU = 1-GPU.
@@ -378,3 +444,25 @@ bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root) {
 }
 
 }  // extern "C"
+
+// Waits for the gather stream (Flush) / frees the frame-output state
+// (DestroyRenderContext).
+void nr_dist_sync(RenderContext* ctx) {
+    if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
+}
+
+void nr_dist_release(RenderContext* ctx) {
+    nr_dist_sync(ctx);
+    for (int x = 0; x < 2; ++x) {
+        if (ctx->frameBuf[x]) NR_CHECK(hipFree(ctx->frameBuf[x]));
+        if (ctx->stageBuf[x]) NR_CHECK(hipFree(ctx->stageBuf[x]));
+        if (ctx->evGatherDone[x]) NR_CHECK(hipEventDestroy(ctx->evGatherDone[x]));
+        ctx->frameBuf[x] = ctx->stageBuf[x] = nullptr;
+        ctx->evGatherDone[x] = nullptr;
+    }
+    ctx->frameU8 = nullptr;
+    if (ctx->evFrameReady) NR_CHECK(hipEventDestroy(ctx->evFrameReady));
+    if (ctx->commStream) NR_CHECK(hipStreamDestroy(ctx->commStream));
+    ctx->evFrameReady = nullptr;
+    ctx->commStream = nullptr;
+}

@@ -290,13 +290,22 @@ def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha)
     R.RenderContext.gather_frame_u8_local(ctxs, root)
     got = ctxs[root].get_frame_u8()
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
-    # a second frame through the same staging buffers
-    for ctx in ctxs:
-        ctx.fill_color(0.5, 0.25, 0.75, 0.5)
-    ref.fill_color(0.5, 0.25, 0.75, 0.5)
-    ref.gather_frame_u8()
-    R.RenderContext.gather_frame_u8_local(ctxs, root)
-    assert np.array_equal(ctxs[root].get_frame_u8(), ref.get_frame_u8())
+    # more frames: the assembly alternates between two frame buffers and
+    # overlaps the next frame (gather stream), so frames 3+ reuse buffers
+    # whose earlier transfer must have finished
+    for f in range(4):
+        for ctx in (ref, *ctxs):
+            if f % 2:
+                ctx.fill_color(0.5, 0.25 * f, 0.75, 0.5)
+            else:
+                ctx.set_color(0.1 * f, 0.2, 0.3, 1.0)
+                ctx.clear_depth()
+                ctx.draw_triangles(xy[f * 300:], c[f * 300:], z=z[f * 300:])
+        ref.gather_frame_u8()
+        R.RenderContext.gather_frame_u8_local(ctxs, root)
+        got = ctxs[root].get_frame_u8()
+        want = ref.get_frame_u8()
+        assert np.array_equal(got, want), (f, np.argwhere(got != want)[:5])
 
 
 def test_single_rank_comm_gather(gpu):
