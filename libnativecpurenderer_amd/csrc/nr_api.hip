@@ -54,6 +54,16 @@ void ClearLastError() {
 #ifndef NR_MAIN_PRIO
 #define NR_MAIN_PRIO 1   // main stream at the greatest priority
 #endif
+// Stream priorities (NR_STREAM_PRIO): 0 main stream above the binning
+// stream, 1 binning above main, 2 both at the least priority.
+static int stream_prio_mode() {
+    static const int v = [] {
+        const char* e = getenv("NR_STREAM_PRIO");
+        const int x = e ? atoi(e) : -1;
+        return x >= 0 && x <= 2 ? x : 0;
+    }();
+    return v;
+}
 static std::mutex g_dev_mu;
 static std::vector<hipStream_t> g_streams;
 
@@ -64,7 +74,8 @@ hipStream_t nr_stream_for(int device) {
         NR_CHECK(hipSetDevice(device));
         int least = 0, greatest = 0;
         NR_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        NR_CHECK(hipStreamCreateWithPriority(&g_streams[device], hipStreamNonBlocking, NR_MAIN_PRIO ? greatest : least));
+        NR_CHECK(hipStreamCreateWithPriority(&g_streams[device], hipStreamNonBlocking,
+                                             stream_prio_mode() == 0 && NR_MAIN_PRIO ? greatest : least));
     }
     return g_streams[device];
 }
@@ -79,7 +90,8 @@ hipStream_t nr_bin_stream_for(int device) {
         NR_CHECK(hipSetDevice(device));
         int least = 0, greatest = 0;
         NR_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        NR_CHECK(hipStreamCreateWithPriority(&g_bin_streams[device], hipStreamNonBlocking, least));
+        NR_CHECK(hipStreamCreateWithPriority(&g_bin_streams[device], hipStreamNonBlocking,
+                                             stream_prio_mode() == 1 ? greatest : least));
     }
     return g_bin_streams[device];
 }

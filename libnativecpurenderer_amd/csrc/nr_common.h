@@ -57,7 +57,7 @@ struct TriScratch {
         hipEvent_t evBin = nullptr;         // binning done (binning stream)
         hipEvent_t evVis = nullptr;         // k_vis done reading the set (main stream)
         bool visRecorded = false;
-    } fset[2];
+    } fset[3];
     int fnext = 0;                          // set of the next batch
     u32* fdone = nullptr; size_t fdone_cap = 0;   // split-tile slice counters (k_vis only)
     u64* vis = nullptr; size_t vis_cap = 0; int visNeutral = -1;

@@ -801,6 +801,17 @@ static u32 slice_target() {
     return v;
 }
 
+// Binning output sets in rotation (NR_BIN_SETS, 2 or 3): with k sets the
+// binning of batch b waits only for the raster of batch b - k.
+static int bin_sets() {
+    static const int v = [] {
+        const char* e = getenv("NR_BIN_SETS");
+        const int x = e ? atoi(e) : 0;
+        return x == 2 || x == 3 ? x : 3;
+    }();
+    return v;
+}
+
 static hipEvent_t sync_event() {
     hipEvent_t e;
     NR_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
@@ -975,7 +986,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable) {
     const bool exact = fp.fragCounter != nullptr;
     TriScratch& sc = ctx->tri;
     const int si = sc.fnext;
-    sc.fnext ^= 1;
+    sc.fnext = (sc.fnext + 1) % bin_sets();
     u32 seq = 0;
     if (!free_enqueue(ctx, src, fp, bp, exact, si, immutable && !exact, &seq)) return;
     if (!exact) {
