@@ -17,6 +17,8 @@ from libnativecpurenderer_amd import _lib  # noqa: E402
 cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c3"]
 xy, z, c = bench.make_scene(cfg)
 ctx = R.RenderContext(cfg["W"], cfg["H"], False)
+if int(os.environ.get("ITEM_SHARDS", "1")) > 1:
+    ctx.set_shard(int(os.environ["ITEM_SHARDS"]), 0)
 buf = R.TriangleBuffer(xy, c, z=z)
 for _ in range(4):
     ctx.set_color(0, 0, 0, 0)
@@ -56,5 +58,11 @@ edges = np.arange(0, span + 2, 2.0)
 act = np.zeros(len(edges))
 for i, t in enumerate(edges):
     act[i] = ((s <= t) & (e > t)).sum()
+order = np.argsort(-e)[:8]
+print("last-finishing items (start, end, tris, slices):",
+      "; ".join(f"{s[i]:.1f}-{e[i]:.1f} n={ntri[i]} sl={nsl[i]}" for i in order))
+order = np.argsort(-dur)[:8]
+print("longest items (start, end, tris, slices):",
+      "; ".join(f"{s[i]:.1f}-{e[i]:.1f} n={ntri[i]} sl={nsl[i]}" for i in order))
 print("active items every 2 us:", " ".join(str(int(x)) for x in act[::2]))
 np.save(os.path.join(ROOT, "gpurun_out", "item_times.npy"), a)

@@ -59,9 +59,9 @@ PATCHES = {
          "            if (r0 >= r1) continue;\n            if (EXP_NOROWS) { if (r1 > 1000) key[0] = r0; continue; }\n"),
     ],
     "EXP_NOPIX": [
-        ("                if (xs >= xe) continue;\n                if (ZMODE == 0) {",
-         "                if (xs >= xe) continue;\n                if (EXP_NOPIX) { if (xe > 100) key[0] = xe; continue; }\n"
-         "                if (ZMODE == 0) {"),
+        ("                    if (xs >= xe) continue;\n                    if (ZMODE == 0) {",
+         "                    if (xs >= xe) continue;\n                    if (EXP_NOPIX) { if (xe > 100) key[0] = xe; continue; }\n"
+         "                    if (ZMODE == 0) {"),
     ],
     "EXP_NOSHADE": [
         ("        if (!multi) {   // the whole list was in this slice: shade now\n",
