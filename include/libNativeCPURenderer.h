@@ -121,6 +121,9 @@ bool GetCommUniqueId(iu8* out128);              /* rank 0: 128-byte RCCL id to d
 NrComm* CreateComm(i64 nranks, i64 rank, const iu8* id128); /* on the current device */
 void DestroyComm(NrComm* comm);
 void SetShard(RenderContext* ctx, i64 nshards, i64 shard);  /* own tile rows ty % nshards == shard */
+void SetShardSlots(RenderContext* ctx, i64 nshards, i64 shard, const i64* slots); /* weighted: rank p owns slots[p]
+                                                 of every sum(slots) <= 64 bands, interleaved (same call on all ranks) */
+i64 GetShardPattern(RenderContext* ctx, iu8* out64);   /* band b -> rank out64[b % period]; returns the period */
 bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root);  /* u8 frame (cpp:52-57) assembled on root */
 void GetFrameU8(RenderContext* ctx, iu8* out);
 void* GetFrameU8DevicePtr(RenderContext* ctx);

@@ -97,6 +97,8 @@ DEVICE_ABI = {
     "CreateComm": (P, (L, L, P)),
     "DestroyComm": (None, (P,)),
     "SetShard": (None, (P, L, L)),
+    "SetShardSlots": (None, (P, L, L, P)),
+    "GetShardPattern": (L, (P, P)),
     "GatherFrameU8": (B, (P, P, L)),
     "GetFrameU8": (None, (P, P)),
     "GetFrameU8DevicePtr": (P, (P,)),

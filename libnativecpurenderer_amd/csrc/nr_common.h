@@ -107,6 +107,11 @@ struct RenderContext {
     iu8* u8buf = nullptr; size_t u8cap = 0;   // GetBufferAsUInt8 staging
     // multi-GPU: owned tile rows ty % nshards == shard (nr_dist.hip)
     int nshards = 1, shard = 0;
+    // band ownership: band b belongs to rank shardPattern[b % shardPeriod]
+    // (SetShard: period nshards, pattern 0..n-1; SetShardSlots: a weighted
+    // interleave); every rank of a frame holds the same pattern
+    int shardPeriod = 1;
+    unsigned char shardPattern[64] = {0};
     // u8 frame output (GatherFrameU8, nr_dist.hip): two frame buffers, the
     // next frame renders into one while the other is assembled on the gather
     // stream; frameU8 = frameBuf[frameCur]
@@ -149,6 +154,7 @@ struct TriangleBuffer {
 // host helpers shared across translation units
 Texture* nr_new_texture(i64 w, i64 h, bool alpha);   // device texels, current device
 void nr_dist_sync(RenderContext* ctx);      // wait for the frame-assembly stream
+u64 nr_shard_mask(const RenderContext* ctx, int rank);   // bit k: pattern slot k belongs to rank
 void nr_dist_release(RenderContext* ctx);   // free the frame-output buffers
 hipStream_t nr_stream_for(int device);
 hipStream_t nr_bin_stream_for(int device);        // second stream: triangle binning overlapped with the raster

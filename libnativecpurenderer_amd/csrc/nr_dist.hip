@@ -76,10 +76,30 @@ bool nccl_ok(Rccl* r, ncclResult_t e, const char* what) {
     return false;
 }
 
-// f64 -> u8 (cpp:52-57) over the owned tile rows only
+// Band ownership of a sharded frame, by value into the kernels: band b
+// belongs to rank pattern[b % period].
+struct ShardMap {
+    int period;
+    unsigned char pattern[64];
+};
+
+// Position of band b among the bands of its owner (bands packed back to back).
+__device__ __forceinline__ i64 band_index(const ShardMap& sm, i64 b, int owner) {
+    const int slot = (int)(b % sm.period);
+    int per = 0, before = 0;
+    for (int k = 0; k < sm.period; ++k) {
+        const bool mine = sm.pattern[k] == owner;
+        per += mine;
+        before += (mine && k < slot);
+    }
+    return (b / sm.period) * per + before;
+}
+
+// f64 -> u8 (cpp:52-57) over the owned tile rows only (grid.y = every band)
 __global__ void k_to_u8_rows(const f64* __restrict__ src, iu8* __restrict__ dst, i64 rowElems, i64 H, int TH,
-                             int nshards, int shard) {
-    const i64 band = (i64)blockIdx.y * nshards + shard;   // owned band index
+                             int period, u64 mask) {
+    const i64 band = blockIdx.y;
+    if (period > 1 && !((mask >> (band % period)) & 1ull)) return;
     const i64 r0 = band * TH;
     if (r0 >= H) return;
     const i64 rows = (H - r0) < TH ? (H - r0) : TH;
@@ -91,11 +111,25 @@ __global__ void k_to_u8_rows(const f64* __restrict__ src, iu8* __restrict__ dst,
 
 constexpr int BAND = 32;   // = nrtri::TH, the tile height
 
-// Rows of the frame owned by `rank` of n (bands b with b % n == rank).
-i64 owned_rows(i64 H, int n, int rank) {
+ShardMap shard_map(const RenderContext* ctx) {
+    ShardMap m;
+    m.period = ctx->shardPeriod;
+    memcpy(m.pattern, ctx->shardPattern, sizeof m.pattern);
+    return m;
+}
+
+// Rows of the frame owned by `rank` under the context's band pattern.
+i64 owned_rows(const RenderContext* ctx, int rank) {
     i64 rows = 0;
-    for (i64 b = rank; b * BAND < H; b += n) rows += std::min<i64>(BAND, H - b * BAND);
+    for (i64 b = 0; b * BAND < ctx->height; ++b)
+        if (ctx->shardPattern[b % ctx->shardPeriod] == rank) rows += std::min<i64>(BAND, ctx->height - b * BAND);
     return rows;
+}
+
+i64 max_owned_rows(const RenderContext* ctx, int n) {
+    i64 m = 0;
+    for (int p = 0; p < n; ++p) m = std::max(m, owned_rows(ctx, p));
+    return m;
 }
 
 // Packed band layout of the gather: a rank's owned bands back to back (its
@@ -104,16 +138,16 @@ i64 owned_rows(i64 H, int n, int rank) {
 // frame into `stage`.  Unpack: the bands of every rank but `root` from its
 // slot of `stage` (rank p at p * peerStride) into the frame.
 template <typename V, bool UNPACK>
-__global__ void k_band_copy(iu8* __restrict__ frame, iu8* __restrict__ stage, i64 rowElems, i64 H, int nranks,
+__global__ void k_band_copy(iu8* __restrict__ frame, iu8* __restrict__ stage, i64 rowElems, i64 H, ShardMap sm,
                             int sel, i64 peerStride) {
     const i64 b = blockIdx.y;
-    const int owner = (int)(b % nranks);
+    const int owner = sm.pattern[b % sm.period];
     if (UNPACK ? owner == sel : owner != sel) return;
     const i64 r0 = b * BAND;
     const i64 rows = (H - r0) < BAND ? (H - r0) : BAND;
     const i64 n = rows * rowElems / (i64)sizeof(V);
     V* f = reinterpret_cast<V*>(frame + r0 * rowElems);
-    V* s = reinterpret_cast<V*>(stage + (UNPACK ? owner * peerStride : 0) + (b / nranks) * BAND * rowElems);
+    V* s = reinterpret_cast<V*>(stage + (UNPACK ? owner * peerStride : 0) + band_index(sm, b, owner) * BAND * rowElems);
     for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
         if (UNPACK) f[i] = s[i];
         else s[i] = f[i];
@@ -122,22 +156,23 @@ __global__ void k_band_copy(iu8* __restrict__ frame, iu8* __restrict__ stage, i6
 
 // Launches k_band_copy over every band on `st` (16-byte vectors when the row
 // length keeps every band 16-byte aligned).
-void band_copy(RenderContext* ctx, iu8* frame, iu8* stage, hipStream_t st, bool unpack, int nranks, int sel,
-               i64 peerStride, i64 rowElems) {
+void band_copy(RenderContext* ctx, iu8* frame, iu8* stage, hipStream_t st, bool unpack, int sel, i64 peerStride,
+               i64 rowElems) {
+    const ShardMap sm = shard_map(ctx);
     const i64 bands = (ctx->height + BAND - 1) / BAND;
     const bool vec = rowElems % 16 == 0;
     const i64 per = BAND * rowElems / (vec ? 16 : 1);
     dim3 grid((unsigned)std::min<i64>((per + 255) / 256, 1024), (unsigned)bands);
     if (vec) {
         if (unpack) hipLaunchKernelGGL((k_band_copy<uint4, true>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                       ctx->height, nranks, sel, peerStride);
+                                       ctx->height, sm, sel, peerStride);
         else hipLaunchKernelGGL((k_band_copy<uint4, false>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                ctx->height, nranks, sel, peerStride);
+                                ctx->height, sm, sel, peerStride);
     } else {
         if (unpack) hipLaunchKernelGGL((k_band_copy<iu8, true>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                       ctx->height, nranks, sel, peerStride);
+                                       ctx->height, sm, sel, peerStride);
         else hipLaunchKernelGGL((k_band_copy<iu8, false>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                ctx->height, nranks, sel, peerStride);
+                                ctx->height, sm, sel, peerStride);
     }
     NR_CHECK(hipGetLastError());
 }
@@ -212,16 +247,16 @@ bool frame_u8_local(RenderContext* ctx) {
     }
     const i64 rowElems = ctx->width * ipp;
     const i64 bands = (ctx->height + BAND - 1) / BAND;
-    const i64 owned = (bands - ctx->shard + ctx->nshards - 1) / ctx->nshards;
+    const i64 owned = owned_rows(ctx, ctx->shard);
     // later triangle resolves write the u8 frame themselves (no re-read of
     // the f64 frame); convert here only when that mirror is not current
     ctx->frameOutput = true;
     if (owned > 0 && !ctx->frameU8Valid) {
-        dim3 grid((unsigned)std::min<i64>((BAND * rowElems + 255) / 256, 4096), (unsigned)owned);
+        dim3 grid((unsigned)std::min<i64>((BAND * rowElems + 255) / 256, 4096), (unsigned)bands);
         hipEvent_t e0, e1;
         nr_timing_begin(ctx, NRK_OUTPUT, &e0, &e1);
         hipLaunchKernelGGL(k_to_u8_rows, grid, dim3(256), 0, ctx->stream, ctx->buffer, ctx->frameU8, rowElems,
-                           ctx->height, BAND, ctx->nshards, ctx->shard);
+                           ctx->height, BAND, ctx->shardPeriod, nr_shard_mask(ctx, ctx->shard));
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_OUTPUT, e0, e1);
     }
@@ -279,8 +314,60 @@ void SetShard(RenderContext* ctx, i64 nshards, i64 shard) {
         nr_set_error_msg("SetShard: need 0 <= shard < nshards");
         return;
     }
+    if (nshards > 64) {
+        nr_set_error_msg("SetShard: at most 64 shards");
+        return;
+    }
     ctx->nshards = (int)nshards;
     ctx->shard = (int)shard;
+    ctx->shardPeriod = (int)nshards;
+    for (int k = 0; k < 64; ++k) ctx->shardPattern[k] = (unsigned char)(k < nshards ? k : 0);
+    ctx->frameU8Valid = false;
+}
+
+// NEW: weighted shards.  Rank p owns slots[p] of every sum(slots) (<= 64)
+// consecutive bands, spread by smooth weighted round robin (each step every
+// rank gains its slots, the rank with the most credit -- lowest rank on ties
+// -- takes the band and pays the period), so a rank's bands are interleaved
+// over the frame.  Equal slots give SetShard's pattern.  Every rank of a
+// frame must make the same call (with its own `shard`).
+void SetShardSlots(RenderContext* ctx, i64 nshards, i64 shard, const i64* slots) {
+    if (nshards < 1 || nshards > 64 || shard < 0 || shard >= nshards) {
+        nr_set_error_msg("SetShardSlots: need 0 <= shard < nshards <= 64");
+        return;
+    }
+    i64 period = 0;
+    for (i64 p = 0; p < nshards; ++p) {
+        if (slots[p] < 1) {
+            nr_set_error_msg("SetShardSlots: every rank needs at least one slot");
+            return;
+        }
+        period += slots[p];
+    }
+    if (period > 64) {
+        nr_set_error_msg("SetShardSlots: sum(slots) must be <= 64");
+        return;
+    }
+    i64 credit[64] = {0};
+    for (i64 k = 0; k < period; ++k) {
+        int best = 0;
+        for (i64 p = 0; p < nshards; ++p) {
+            credit[p] += slots[p];
+            if (credit[p] > credit[best]) best = (int)p;
+        }
+        credit[best] -= period;
+        ctx->shardPattern[k] = (unsigned char)best;
+    }
+    ctx->nshards = (int)nshards;
+    ctx->shard = (int)shard;
+    ctx->shardPeriod = (int)period;
+    ctx->frameU8Valid = false;
+}
+
+// NEW: the band pattern (period entries, owner rank per band slot).
+i64 GetShardPattern(RenderContext* ctx, iu8* out64) {
+    memcpy(out64, ctx->shardPattern, 64);
+    return ctx->shardPeriod;
 }
 
 // NEW: the u8 image of the frame (cpp:52-57 per element) assembled on `root`
@@ -308,21 +395,21 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
     // overlap the next frame, which renders into the other frame buffer.
     const int n = comm->nranks, me = comm->rank, x = ctx->frameCur;
     const i64 rowElems = ctx->width * (ctx->enableAlpha ? 4 : 3);
-    const i64 peerStride = owned_rows(ctx->height, n, 0) * rowElems;   // rank 0 owns the most bands
+    const i64 peerStride = max_owned_rows(ctx, n) * rowElems;
     ensure_comm_stream(ctx);
-    if (!ensure_stage(ctx, x, (size_t)(me == root ? n * peerStride : owned_rows(ctx->height, n, me) * rowElems)))
+    if (!ensure_stage(ctx, x, (size_t)(me == root ? n * peerStride : owned_rows(ctx, me) * rowElems)))
         return false;
     iu8* frame = ctx->frameBuf[x];
     iu8* stage = ctx->stageBuf[x];
     hipEvent_t e0, e1;
     nr_timing_begin(ctx, NRK_GATHER, &e0, &e1);
-    if (me != root) band_copy(ctx, frame, stage, ctx->stream, false, n, me, 0, rowElems);
+    if (me != root) band_copy(ctx, frame, stage, ctx->stream, false, me, 0, rowElems);
     nr_timing_end(ctx, NRK_GATHER, e0, e1);
     NR_CHECK(hipEventRecord(ctx->evFrameReady, ctx->stream));
     NR_CHECK(hipStreamWaitEvent(ctx->commStream, ctx->evFrameReady, 0));
     bool ok = nccl_ok(r, r->GroupStart(), "ncclGroupStart");
     for (int p = 0; p < n && ok; ++p) {
-        const size_t cnt = (size_t)(owned_rows(ctx->height, n, p) * rowElems);
+        const size_t cnt = (size_t)(owned_rows(ctx, p) * rowElems);
         if (cnt == 0) continue;
         if (me == root && p != root)
             ok = nccl_ok(r, r->Recv(stage + p * peerStride, cnt, ncclUint8, p, comm->comm, ctx->commStream),
@@ -331,7 +418,7 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
             ok = nccl_ok(r, r->Send(stage, cnt, ncclUint8, (int)root, comm->comm, ctx->commStream), "ncclSend");
     }
     ok = nccl_ok(r, r->GroupEnd(), "ncclGroupEnd") && ok;
-    if (ok && me == root) band_copy(ctx, frame, stage, ctx->commStream, true, n, (int)root, peerStride, rowElems);
+    if (ok && me == root) band_copy(ctx, frame, stage, ctx->commStream, true, (int)root, peerStride, rowElems);
     rotate_frame(ctx, x);
     return ok;
 }
@@ -350,8 +437,9 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     for (i64 p = 0; p < n; ++p) {
         RenderContext* c = ctxs[p];
         if (c->nshards != n || c->shard != p || c->width != rc->width || c->height != rc->height ||
-            c->enableAlpha != rc->enableAlpha || c->device != rc->device) {
-            nr_set_error_msg("GatherFrameU8Local: ctxs[p] must be shard p of n, all of one size and device");
+            c->enableAlpha != rc->enableAlpha || c->device != rc->device || c->shardPeriod != rc->shardPeriod ||
+            memcmp(c->shardPattern, rc->shardPattern, 64) != 0) {
+            nr_set_error_msg("GatherFrameU8Local: ctxs[p] must be shard p of n (one pattern), all of one size and device");
             return false;
         }
         NR_CHECK(hipSetDevice(c->device));
@@ -359,7 +447,7 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     }
     if (n == 1) return true;
     const i64 rowElems = rc->width * (rc->enableAlpha ? 4 : 3);
-    const i64 peerStride = owned_rows(rc->height, (int)n, 0) * rowElems;
+    const i64 peerStride = max_owned_rows(rc, (int)n) * rowElems;
     NR_CHECK(hipSetDevice(rc->device));
     ensure_comm_stream(rc);
     const int xr = rc->frameCur;
@@ -369,9 +457,9 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
         RenderContext* c = ctxs[p];
         ensure_comm_stream(c);
         const int xp = c->frameCur;
-        const size_t cnt = (size_t)(owned_rows(c->height, (int)n, (int)p) * rowElems);
+        const size_t cnt = (size_t)(owned_rows(c, (int)p) * rowElems);
         if (!ensure_stage(c, xp, cnt)) return false;
-        band_copy(c, c->frameBuf[xp], c->stageBuf[xp], c->stream, false, (int)n, (int)p, 0, rowElems);
+        band_copy(c, c->frameBuf[xp], c->stageBuf[xp], c->stream, false, (int)p, 0, rowElems);
         NR_CHECK(hipEventRecord(c->evFrameReady, c->stream));
         NR_CHECK(hipStreamWaitEvent(rc->commStream, c->evFrameReady, 0));
         NR_CHECK(hipMemcpyAsync(rc->stageBuf[xr] + p * peerStride, c->stageBuf[xp], cnt, hipMemcpyDeviceToDevice,
@@ -379,7 +467,7 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     }
     NR_CHECK(hipEventRecord(rc->evFrameReady, rc->stream));
     NR_CHECK(hipStreamWaitEvent(rc->commStream, rc->evFrameReady, 0));
-    band_copy(rc, rc->frameBuf[xr], rc->stageBuf[xr], rc->commStream, true, (int)n, (int)root, peerStride, rowElems);
+    band_copy(rc, rc->frameBuf[xr], rc->stageBuf[xr], rc->commStream, true, (int)root, peerStride, rowElems);
     // the peers' stages were read on the root's gather stream: their own
     // gather streams (whose events guard the buffers' reuse) wait for it
     NR_CHECK(hipEventRecord(rc->evGatherDone[xr], rc->commStream));
@@ -427,7 +515,7 @@ bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root) {
     const i64 bands = (ctx->height + BAND - 1) / BAND;
     bool ok = nccl_ok(r, r->GroupStart(), "ncclGroupStart");
     for (i64 b = 0; b < bands && ok; ++b) {
-        const int owner = (int)(b % comm->nranks);
+        const int owner = ctx->shardPattern[b % ctx->shardPeriod];
         const i64 rows = std::min<i64>(BAND, ctx->height - b * BAND);
         f64* p = ctx->buffer + b * BAND * rowElems;
         u32* d = ctx->depth ? ctx->depth + b * BAND * ctx->width : nullptr;
@@ -465,4 +553,12 @@ void nr_dist_release(RenderContext* ctx) {
     if (ctx->commStream) NR_CHECK(hipStreamDestroy(ctx->commStream));
     ctx->evFrameReady = nullptr;
     ctx->commStream = nullptr;
+}
+
+u64 nr_shard_mask(const RenderContext* ctx, int rank) {
+    if (ctx->shardPeriod <= 1) return 1ull;
+    u64 m = 0;
+    for (int k = 0; k < ctx->shardPeriod; ++k)
+        if (ctx->shardPattern[k] == rank) m |= 1ull << k;
+    return m;
 }

@@ -35,13 +35,13 @@ struct BinParams {
     f64 m[6];
     i64 W, H;
     int tiles_x;
-    int nshards, shard;   // owned tile rows: ty % nshards == shard
+    int period;           // owned tile rows: bit (ty % period) of mask (SetShard / SetShardSlots)
+    u64 mask;
 };
 
 // (unsharded: no integer division -- it costs ~30 VALU instructions)
-__device__ __forceinline__ bool owned_row(int ty, int nshards, int shard) { return nshards == 1 || ty % nshards == shard; }
-__device__ __forceinline__ bool owned_tile(int tile, int tiles_x, int nshards, int shard) {
-    return nshards == 1 || (tile / tiles_x) % nshards == shard;
+__device__ __forceinline__ bool owned_row(int ty, int period, u64 mask) {
+    return period == 1 || ((mask >> (ty % period)) & 1ull);
 }
 
 __device__ __forceinline__ f64 clampd(f64 v, f64 lo, f64 hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -225,7 +225,8 @@ struct FrameParams {
     i64 W, H;
     int ipp;
     int tiles_x, tiles_y;
-    int nshards, shard;
+    int period;   // owned tile rows (BinParams)
+    u64 mask;
     int depthTest, depthWrite;
     int pendColor;
     f64 pendColorValue;

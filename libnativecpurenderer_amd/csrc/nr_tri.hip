@@ -40,8 +40,8 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src) {
     fp.ipp = ctx->enableAlpha ? 4 : 3;
     fp.tiles_x = (int)((ctx->width + TW - 1) / TW);
     fp.tiles_y = (int)((ctx->height + TH - 1) / TH);
-    fp.nshards = ctx->nshards;
-    fp.shard = ctx->shard;
+    fp.period = ctx->shardPeriod;
+    fp.mask = nr_shard_mask(ctx, ctx->shard);
     fp.depthTest = ctx->depthTest;
     fp.depthWrite = ctx->depthWrite;
     fp.pendColor = ctx->pendColor;

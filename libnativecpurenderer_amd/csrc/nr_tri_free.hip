@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
         rects[t] = hit ? pack_rect(tx0, tx1, ty0, ty1) : NO_RECT;
         if (!hit) continue;
         for (int ty = ty0; ty <= ty1; ++ty) {
-            if (!owned_row(ty, bp.nshards, bp.shard)) continue;
+            if (!owned_row(ty, bp.period, bp.mask)) continue;
             for (int tx = tx0; tx <= tx1; ++tx) {
                 const int bin = ty * bp.tiles_x + tx;
                 if (LDSH) atomicAdd(&hist[bin], 1u);
@@ -144,8 +144,8 @@ __device__ __forceinline__ int size_class(u32 c, u32 slice) {
 
 // Tiles are taken PLAN_T at a time (thread = tile: coalesced), each round a
 // workgroup scan carried over from the previous one.
-__global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int nshards,
-                                                      int shard, u32* __restrict__ off, uint4* __restrict__ items,
+__global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
+                                                      u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
                                                       u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
                                                       u32 slice_target) {
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     u32 b = 0, m = 0;
     for (int i = tid; i < ntiles; i += PLAN_T) {
         const u32 c = cnt[i];
-        const u32 ni = tile_items(c, owned_row(i / tiles_x, nshards, shard), slice);
+        const u32 ni = tile_items(c, owned_row(i / tiles_x, period, mask), slice);
         b += ni;
         m += c > slice ? 1u : 0u;
         if (ni) atomicAdd(&bcnt[size_class(c, slice)], ni);
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         u32 c = 0, ni = 0;
         if (i < ntiles) {
             c = cnt[i];
-            ni = tile_items(c, owned_row(i / tiles_x, nshards, shard), slice);
+            ni = tile_items(c, owned_row(i / tiles_x, period, mask), slice);
         }
         const u32 ia = wave_scan(c, lane);
         if (lane == 63) sh[0][w] = ia;
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
             const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
             const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
             for (int ty = ty0; ty <= ty1; ++ty)
-                if (owned_row(ty, bp.nshards, bp.shard))
+                if (owned_row(ty, bp.period, bp.mask))
                     for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * bp.tiles_x + tx], 1u);
         }
         __syncthreads();
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
         const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
         const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
         for (int ty = ty0; ty <= ty1; ++ty) {
-            if (!owned_row(ty, bp.nshards, bp.shard)) continue;
+            if (!owned_row(ty, bp.period, bp.mask)) continue;
             for (int tx = tx0; tx <= tx1; ++tx) {
                 const int bin = ty * bp.tiles_x + tx;
                 const u32 slot = LDSH ? atomicAdd(&hist[bin], 1u) : off[bin] + atomicAdd(&cur[bin], 1u);
@@ -922,8 +922,8 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.nshards,
-                           fp.shard, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
+        hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
+                           fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
                            (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_SCAN, e0, e1, sb);
@@ -981,7 +981,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable) {
     bp.src = src;
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
-    bp.nshards = fp.nshards; bp.shard = fp.shard;
+    bp.period = fp.period; bp.mask = fp.mask;
     // fragment counting reads a counter back anyway: run exact (synchronous)
     const bool exact = fp.fragCounter != nullptr;
     TriScratch& sc = ctx->tri;

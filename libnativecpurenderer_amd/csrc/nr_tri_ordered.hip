@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned 
     unsigned long long c = 0;
     if (tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) {
         int rows = 0;
-        for (int ty = ty0; ty <= ty1; ++ty) rows += owned_row(ty, bp.nshards, bp.shard) ? 1 : 0;
+        for (int ty = ty0; ty <= ty1; ++ty) rows += owned_row(ty, bp.period, bp.mask) ? 1 : 0;
         c = (unsigned long long)(tx1 - tx0 + 1) * rows;
     }
     cnt[t] = c;
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_tri_emit(const BinParams bp, const unsi
     if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) return;
     unsigned long long o = off[t];
     for (int ty = ty0; ty <= ty1; ++ty)
-        if (owned_row(ty, bp.nshards, bp.shard))
+        if (owned_row(ty, bp.period, bp.mask))
         for (int tx = tx0; tx <= tx1; ++tx) {
             keys[o] = (u32)(ty * bp.tiles_x + tx);
             vals[o] = (u32)t;
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
     const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (!owned_row(ty, fp.nshards, fp.shard)) return;
+    if (!owned_row(ty, fp.period, fp.mask)) return;
     const u32 ls = tstart[tile], le = tend[tile];
     if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
 
@@ -295,7 +295,7 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
     bp.src = src;
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
-    bp.nshards = fp.nshards; bp.shard = fp.shard;
+    bp.period = fp.period; bp.mask = fp.mask;
 
     u64* tri_bufs[2] = {sc.cnt, sc.off};
     if (!grow_set(tri_bufs, &sc.tri_cap, (size_t)src.n)) return;

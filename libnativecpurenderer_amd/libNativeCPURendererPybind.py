@@ -318,6 +318,21 @@ class RenderContext:
         """Render only the 32-pixel tile rows ty with ty % nshards == shard."""
         lib.SetShard(self._ptr, nshards, shard)
 
+    def set_shard_slots(self, nshards: int, shard: int, slots: typing.Sequence[int]):
+        """Weighted shards: rank p owns slots[p] of every sum(slots) (<= 64)
+        tile rows, interleaved (SetShardSlots).  Same call on every rank."""
+        arr = (ctypes.c_long * nshards)(*[int(v) for v in slots])
+        lib.SetShardSlots(self._ptr, nshards, shard, arr)
+        err = _lib.last_error()
+        if "SetShardSlots" in err:
+            raise ValueError(err)
+
+    def get_shard_pattern(self) -> typing.List[int]:
+        """Owner rank of tile row ty is pattern[ty % len(pattern)]."""
+        buf = (ctypes.c_ubyte * 64)()
+        period = lib.GetShardPattern(self._ptr, buf)
+        return list(buf[:period])
+
     def gather_frame_u8(self, comm: typing.Optional["Comm"] = None, root: int = 0):
         """u8 image of the frame assembled on `root` (local conversion when
         comm is None).  Asynchronous; read it with get_frame_u8()."""

@@ -13,23 +13,46 @@ import numpy as np
 TILE_H = 32
 
 
-def owned_bands(height: int, nshards: int, shard: int, tile_h: int = TILE_H):
+def band_pattern(nshards: int, slots=None):
+    """Owner rank of each band slot; band b belongs to pattern[b % len(pattern)].
+    Equal shards (slots None): 0..n-1 (SetShard).  Weighted: smooth weighted
+    round robin over sum(slots) slots, lowest rank on ties (SetShardSlots,
+    nr_dist.hip) -- the same integer algorithm, so host and device agree."""
+    if slots is None:
+        return list(range(nshards))
+    slots = [int(v) for v in slots]
+    period = sum(slots)
+    credit = [0] * nshards
+    out = []
+    for _ in range(period):
+        best = 0
+        for p in range(nshards):
+            credit[p] += slots[p]
+            if credit[p] > credit[best]:
+                best = p
+        credit[best] -= period
+        out.append(best)
+    return out
+
+
+def owned_bands(height: int, nshards: int, shard: int, tile_h: int = TILE_H, slots=None):
     """[(y0, y1), ...] half-open row ranges owned by `shard`."""
+    pat = band_pattern(nshards, slots)
     bands = (height + tile_h - 1) // tile_h
-    return [(b * tile_h, min(height, (b + 1) * tile_h)) for b in range(shard, bands, nshards)]
+    return [(b * tile_h, min(height, (b + 1) * tile_h)) for b in range(bands) if pat[b % len(pat)] == shard]
 
 
-def owned_rows(height: int, nshards: int, shard: int, tile_h: int = TILE_H) -> np.ndarray:
-    rows = [np.arange(y0, y1) for y0, y1 in owned_bands(height, nshards, shard, tile_h)]
+def owned_rows(height: int, nshards: int, shard: int, tile_h: int = TILE_H, slots=None) -> np.ndarray:
+    rows = [np.arange(y0, y1) for y0, y1 in owned_bands(height, nshards, shard, tile_h, slots)]
     return np.concatenate(rows) if rows else np.zeros(0, dtype=np.int64)
 
 
-def assemble(parts, height: int, nshards: int, tile_h: int = TILE_H) -> np.ndarray:
+def assemble(parts, height: int, nshards: int, tile_h: int = TILE_H, slots=None) -> np.ndarray:
     """parts[r] = rank r's full-size array, valid on its owned rows; returns
     the assembled frame (rows of each shard taken from its owner)."""
     out = np.empty_like(parts[0])
     for r, a in enumerate(parts):
-        for y0, y1 in owned_bands(height, nshards, r, tile_h):
+        for y0, y1 in owned_bands(height, nshards, r, tile_h, slots):
             out[y0:y1] = a[y0:y1]
     return out
 

@@ -27,6 +27,27 @@ def test_ownership_partitions_rows():
                 assert len(mid) == n
 
 
+def test_weighted_band_patterns():
+    """SetShardSlots' smooth weighted round robin (host restatement): every
+    rank gets exactly slots[p] of each period, equal slots give SetShard's
+    0..n-1, and a rank's bands are spread (no run longer than needed)."""
+    assert sharding.band_pattern(4) == [0, 1, 2, 3]
+    assert sharding.band_pattern(4, [1, 1, 1, 1]) == [0, 1, 2, 3]
+    for slots in ([3, 1], [1, 4, 2], [6, 2, 2, 2, 2, 2, 2, 2], [10, 1, 1]):
+        pat = sharding.band_pattern(len(slots), slots)
+        assert len(pat) == sum(slots)
+        assert [pat.count(p) for p in range(len(slots))] == slots
+        big = max(range(len(slots)), key=lambda p: slots[p])
+        run = max(len(x) for x in "".join("x" if q == big else " " for q in pat).split(" "))
+        others = sum(slots) - slots[big]
+        assert run <= -(-slots[big] // max(1, others)) + 1
+    H = 2160
+    for slots in ([3, 1], [6, 2, 2, 2, 2, 2, 2, 2]):
+        n = len(slots)
+        rows = np.concatenate([sharding.owned_rows(H, n, r, slots=slots) for r in range(n)])
+        assert np.array_equal(np.sort(rows), np.arange(H))
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -218,24 +218,39 @@ def test_order_free_equals_ordered(gpu, mode, gouraud):
     assert_same(outs[0], outs[1], f"free-vs-ordered {mode} g={gouraud}")
 
 
-def _bands(H, n, r, th=32):
-    """Rows owned by shard r of n (tile rows ty % n == r)."""
-    return [y for y in range(H) if (y // th) % n == r]
+def _bands(H, n, r, th=32, slots=None):
+    """Rows owned by shard r of n (tile row ty -> pattern[ty % period])."""
+    from libnativecpurenderer_amd import sharding
+    pat = sharding.band_pattern(n, slots)
+    return [y for y in range(H) if pat[(y // th) % len(pat)] == r]
 
 
-@pytest.mark.parametrize("nshards", [2, 3, 8])
+def _set_shard(ctx, n, r, slots):
+    if slots is None:
+        ctx.set_shard(n, r)
+    else:
+        ctx.set_shard_slots(n, r, slots)
+
+
+@pytest.mark.parametrize("nshards,slots", [(2, None), (3, None), (8, None), (2, [3, 1]), (3, [1, 4, 2]),
+                                           (8, [5, 2, 2, 2, 2, 2, 2, 2])])
 @pytest.mark.parametrize("opaque", [True, False])
-def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, opaque):
-    """Every shard renders only its tile rows; the owned rows of all shards
-    put together are byte-identical to the unsharded frame (colour + depth),
-    for both rasterisers; fragment counts add up."""
+def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque):
+    """Every shard renders only its tile rows (equal shards, or weighted
+    SetShardSlots patterns); the owned rows of all shards put together are
+    byte-identical to the unsharded frame (colour + depth), for both
+    rasterisers; fragment counts add up; the library's band pattern is the
+    host helper's."""
     W, H = 333, 250
     alpha = None if opaque else (0.3, 0.9)
     xy, z, c = scenes.triangle_soup(3000, W, H, 18, seed=41, gouraud=True, alpha=alpha)
 
     def render(n, r):
         ctx = gpu.context(W, H, False)
-        ctx.set_shard(n, r)
+        _set_shard(ctx, n, r, slots if n > 1 else None)
+        if n > 1:
+            from libnativecpurenderer_amd import sharding
+            assert ctx.get_shard_pattern() == sharding.band_pattern(n, slots)
         ctx.set_color(0.1, 0.1, 0.1, 0.1)
         ctx.set_depth_state(True, True)
         ctx.clear_depth()
@@ -249,7 +264,7 @@ def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, opaque):
     frags = 0
     for r in range(nshards):
         f, zz, u8, fr = render(nshards, r)
-        rows = _bands(H, nshards, r)
+        rows = _bands(H, nshards, r, slots=slots)
         asm[rows], asmz[rows], asmu8[rows] = f[rows], zz[rows], u8[rows]
         frags += fr
     assert scenes.bits_equal(asm, full)
@@ -264,9 +279,12 @@ def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, opaque):
     assert np.array_equal(fullu8, ctx.get_buffer_as_uint8_numpy())
 
 
-@pytest.mark.parametrize("nshards,root,W,H,alpha", [(2, 0, 333, 250, False), (3, 1, 333, 250, True),
-                                                     (8, 0, 256, 300, False), (8, 5, 100, 40, False)])
-def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha):
+@pytest.mark.parametrize("nshards,root,W,H,alpha,slots", [(2, 0, 333, 250, False, None), (3, 1, 333, 250, True, None),
+                                                           (8, 0, 256, 300, False, None), (8, 5, 100, 40, False, None),
+                                                           (2, 0, 256, 500, False, [5, 1]),
+                                                           (4, 2, 333, 700, True, [1, 2, 6, 3]),
+                                                           (8, 0, 512, 1000, False, [6, 2, 2, 2, 2, 2, 2, 2])])
+def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha, slots):
     """GatherFrameU8's assembly (each rank's bands packed into one message,
     one unpack on the root), run for n shards on one GPU with device copies in
     place of RCCL: the root's u8 frame equals the unsharded frame byte for
@@ -276,7 +294,7 @@ def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha)
 
     def render(n, r):
         ctx = gpu.context(W, H, alpha)
-        ctx.set_shard(n, r)
+        _set_shard(ctx, n, r, slots if n > 1 else None)
         ctx.set_color(0.2, 0.1, 0.3, 1.0)
         ctx.set_depth_state(True, True)
         ctx.clear_depth()
