@@ -124,17 +124,31 @@ def main():
     ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="experiment: render shard 0 of N on this one GPU (no gather) to time one rank's share")
+    ap.add_argument("--gloo-test", action="store_true",
+                    help="testing the N>1 orchestration on one GPU: gloo process group, CPU reductions, every rank "
+                         "renders its shard on its LOCAL_RANK device but the RCCL frame gather is skipped")
+    ap.add_argument("--root-slots", default="auto",
+                    help="N>1 (and --emulate-shards): tile-row share of rank 0, in bands per 2 bands of every other "
+                         "rank (SetShardSlots); 'equal' = SetShard; 'auto' (N>1) times candidates and keeps the "
+                         "fastest -- the root also receives every other rank's bands, so it gets less to render "
+                         "when the gather dominates")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gloo_test:
+        local_rank = 0   # every rank on the one GPU
     import torch
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.gloo_test:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    rdev = "cpu" if args.gloo_test else "cuda"   # device of the reduction tensors
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     R.set_device(local_rank)
 
@@ -147,12 +161,25 @@ def main():
         ctx.set_force_ordered_raster(True)
     buf = R.TriangleBuffer(xy, c, z=z, gouraud=cfg["gouraud"])
     comm = None
-    if world > 1:
+    nsh = world if world > 1 else max(1, args.emulate_shards)
+    me = rank if world > 1 else 0
+
+    def slots_for(k):
+        return None if k is None else [k] + [2] * (nsh - 1)
+
+    def apply_partition(k):
+        if nsh <= 1:
+            return
+        if k is None:
+            ctx.set_shard(nsh, me)
+        else:
+            ctx.set_shard_slots(nsh, me, slots_for(k))
+
+    fixed_k = None if args.root_slots in ("auto", "equal") else int(args.root_slots)
+    apply_partition(fixed_k)
+    if world > 1 and not args.gloo_test:
         from libnativecpurenderer_amd import sharding
-        ctx.set_shard(world, rank)
         comm = sharding.make_comm(dist, world, rank)
-    elif args.emulate_shards > 1:
-        ctx.set_shard(args.emulate_shards, 0)
 
     def frame():
         ctx.set_color(0, 0, 0, 0)
@@ -168,18 +195,40 @@ def main():
     frags = ctx.get_fragment_count()
     ctx.set_fragment_counting(False)
     if dist is not None:
-        t = torch.tensor([frags], dtype=torch.int64, device="cuda")
+        t = torch.tensor([frags], dtype=torch.int64, device=rdev)
         dist.all_reduce(t)
         frags = int(t.item())
-
-    for _ in range(args.warmup):
-        frame()
-    ctx.flush()
 
     def sync():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
+
+    # partition calibration (N>1, --root-slots auto): every candidate share of
+    # rank 0 is timed over a few frames (max over ranks) and the fastest kept
+    root_k, calib = fixed_k, {}
+    if world > 1 and args.root_slots == "auto":
+        for k in (None, 3, 4, 5, 6, 8, 10, 12):
+            apply_partition(k)
+            for _ in range(3):
+                frame()
+            ctx.flush()
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                frame()
+            ctx.flush()
+            torch.cuda.synchronize()
+            t = torch.tensor([time.perf_counter() - t0], device=rdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            calib["equal" if k is None else str(k)] = round(float(t.item()) / 10 * 1e3, 4)
+        best = min(calib, key=calib.get)
+        root_k = None if best == "equal" else int(best)
+        apply_partition(root_k)
+
+    for _ in range(args.warmup):
+        frame()
+    ctx.flush()
 
     names = ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "vis_init", "tile_raster",
              "resolve", "fill", "output", "gather")
@@ -199,8 +248,7 @@ def main():
             kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
     path = ctx.last_raster_path()
     from libnativecpurenderer_amd import sharding
-    nsh = args.emulate_shards if (world == 1 and args.emulate_shards > 1) else world
-    frac = len(sharding.owned_rows(H, nsh, rank)) / H
+    frac = len(sharding.owned_rows(H, nsh, me, slots=slots_for(root_k) if nsh > 1 else None)) / H
     kb = kernel_bytes(cfg, n_tri, path, frac)
     dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
@@ -218,7 +266,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device="cuda")
+        t = torch.tensor([dt], device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         dist.barrier()
@@ -250,7 +298,9 @@ def main():
                    "fragments_per_frame": int(frags), "frame_pixels": W * H,
                    "parallelism": (f"tile-row shards x{world} + RCCL u8 frame gather" if world > 1
                                    else f"EMULATED shard 0 of {nsh} on one GPU (no gather)" if nsh > 1
-                                   else "single GPU")},
+                                   else "single GPU"),
+                   **({"shard_slots": slots_for(root_k) or "equal", "partition_calibration_ms": calib}
+                      if nsh > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBPS, 4),

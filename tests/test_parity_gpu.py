@@ -436,3 +436,26 @@ def test_hit_effect_needs_alpha_mask(gpu):
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     tex = R.Texture.from_numpy(np.zeros((8, 8, 3), dtype=np.uint8))
     assert not R.lib.CreateMilthmHitEffectTexture(tex._ptr, 0.1, 0.5, 1.0, 1.0, 1.0)
+
+
+def test_bench_multi_rank_orchestration_on_one_gpu(gpu, tmp_path):
+    """bench.py's N>1 path (torchrun, 2 ranks): partition calibration over
+    weighted shards, barriers, max-over-ranks timing and the JSON line -- run
+    with a gloo group and every rank on this one GPU (--gloo-test skips only the
+    RCCL frame gather, which needs one GPU per rank)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(scenes.ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "5", "--warmup", "1", "--gloo-test", "--config", "c2"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 5
+    assert set(d["config"]["partition_calibration_ms"]) >= {"equal", "3", "12"}
