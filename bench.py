@@ -11,10 +11,13 @@ library's fragment counter; equal to the oracle's count — tests check it).
 
 Every step ends with the frame output: the u8 image (cpp:52-57, what the
 video writer consumes) assembled on rank 0.  Multi-GPU (torchrun, one process
-per GPU): the frame's 32-pixel tile rows are owned round-robin by the ranks;
-every rank bins and rasterises only its rows (no data-path collective), then
-its rows of the u8 image go to rank 0 in one grouped RCCL send/recv over xGMI
-(DESIGN.md §5).  At N=1 the same step runs with a local conversion.
+per GPU): the frame's 32-pixel tile rows are owned by the ranks in an
+interleaved pattern; every rank bins and rasterises only its rows (no data-
+path collective), then its rows of the u8 image go to rank 0 as one packed
+RCCL message over xGMI, overlapped with the next frame.  Rank 0
+also receives everyone's rows, so its share of the rows is calibrated before
+the timed region (--root-slots auto: candidate weighted patterns timed, the
+fastest kept and reported).  At N=1 the same step runs with a local conversion.
 value = frame fragments (summed over ranks) x steps / max-over-ranks time.
 
 Prints ONE JSON line on rank 0.
