@@ -63,6 +63,7 @@ struct TriScratch {
     u64* vis = nullptr; size_t vis_cap = 0; int visNeutral = -1;
     u32 planSeq = 0;                        // sequence number of the last async plan
     u64 lastPairs = 0;                      // capacity estimate for the next batch
+    u32 lastHeavy = 0;                      // dense tiles of the last batch (k_vis workgroup size)
     u64 lastN = 0;                          // its triangle count (k_vis variant choice)
     u64 capOverride = 0;                    // testing: force this pair capacity
     int coopMode = 0;                       // k_vis variant: 0 auto, 1 coop, 2 lane-only (SetCoopRaster)

@@ -128,6 +128,7 @@ __device__ __forceinline__ u32 wave_scan(u32 v, int lane) {
 }
 
 constexpr int PLAN_T = 1024, PLAN_W = PLAN_T / 64;
+constexpr u32 HEAVY_PAIRS = 256;   // a dense tile (for the k_vis workgroup-size choice)
 constexpr int PLAN_NB = 12;
 
 // Size class of a tile's work items: 0 empty, 1 + floor(log2(count)) (capped)
@@ -157,14 +158,18 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     // in [SLICE_MIN, SLICE] giving at most ~slice_target items of work
     // (short lists are sliced finer so that a sharded frame, whose dense tiles
     // are few, still fills the chip)
-    u32 a = 0;
-    for (int i = tid; i < ntiles; i += PLAN_T) a += cnt[i];
-    a = wave_scan(a, lane);
-    if (lane == 63) sh[0][w] = a;
+    u32 a = 0, hv = 0;
+    for (int i = tid; i < ntiles; i += PLAN_T) {
+        const u32 c = cnt[i];
+        a += c;
+        hv += c >= HEAVY_PAIRS ? 1u : 0u;
+    }
+    a = wave_scan(a, lane); hv = wave_scan(hv, lane);
+    if (lane == 63) { sh[0][w] = a; sh[1][w] = hv; }
     __syncthreads();
-    u32 ta = 0;
+    u32 ta = 0, th = 0;
 #pragma unroll
-    for (int k = 0; k < PLAN_W; ++k) ta += sh[0][k];
+    for (int k = 0; k < PLAN_W; ++k) { ta += sh[0][k]; th += sh[1][k]; }
     u32 slice = SLICE_MIN;
     while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
     __syncthreads();
@@ -229,6 +234,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
             totals[k] = t[k];
             __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // the batch's sequence number last: the host polls it (nr_settle)
         __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -543,12 +549,15 @@ constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 // two pixels per step).  Then the workgroup shades the tile (shade_tile).
 // COOP: large triangles rasterised by the whole wave (coop pass); the host picks it from the previous batch's
 // pair density -- the variant without it keeps fewer registers live for sliver meshes.
-template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
-__global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES_PER_EU))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
+// NT: workgroup size (VWG, or 2 * VWG for batches with few pairs, whose dense
+// items are latency-bound: more waves per item).
+template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES_PER_EU))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ vis, u32* __restrict__ done,
                                              const u32* __restrict__ plan) {
     constexpr bool DEPTH = ZMODE != 0;
+    constexpr int NWV = NT / 64;   // waves per workgroup
     // tile keys, rows padded to KS = 65 entries: lanes working on different
     // rows at the same column then hit different LDS banks
     // one LDS block (ShadeStage): hash tables | tile keys | extra; the
@@ -579,14 +588,14 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
         const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
         if (ls == le) {   // no triangle: only the pending clears
-            for (int p = tid; p < TH * TW; p += VWG) {
+            for (int p = tid; p < TH * TW; p += NT) {
                 const int lx = p & (TW - 1), ly = p / TW;
                 if (lx < wlim && ly < hlim) store_clear<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx);
             }
             continue;
         }
 
-        for (int p = tid; p < TH * TW; p += VWG) {
+        for (int p = tid; p < TH * TW; p += NT) {
             const int lx = p & (TW - 1), ly = p / TW;
             u32 z0 = 0xFFFFFFFFu;
             if (DEPTH && lx < wlim && ly < hlim)
@@ -604,7 +613,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         // blocks of rows sized to the widest span).  A short slice is cut into NW chunks so that every
         // wave gets a share.
         const u32 ns = le - ls;
-        const u32 cs = ns >= 64u * NW ? 64u : (ns + NW - 1) / NW;
+        const u32 cs = ns >= 64u * NWV ? 64u : (ns + NWV - 1) / NWV;
         const u32 nch = (ns + cs - 1) / cs;
         u32 pt = 0;
         f64 pxy[6], pz[3] = {0, 0, 0};
@@ -620,7 +629,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
             }
         };
         prefetch(wave);
-        for (u32 c = wave; c < nch; c += NW) {
+        for (u32 c = wave; c < nch; c += NWV) {
             const u32 base = ls + c * cs;
             const int cnt = (int)((le - base) < cs ? (le - base) : cs);
             const u32 t = pt;
@@ -628,7 +637,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
 #pragma unroll
             for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
             const f64 zz0 = pz[0], dz1 = pz[1] - pz[0], dz2 = pz[2] - pz[0];
-            prefetch(c + NW);
+            prefetch(c + NWV);
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
             const f64 den = e1x * e2y - e2x * e1y;
             int r0 = 0, r1 = 0;   // rows with a straddling edge: ymin <= y < ymax (exact)
@@ -716,7 +725,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         }
         __syncthreads();
         if (!multi) {   // the whole list was in this slice: shade now
-            shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim, key, lds, nU);
+            shade_tile<ZMODE, GOURAUD, NT>(fp, x0, y0, wlim, hlim, key, lds, nU);
             continue;
         }
         // split tile: merge into the global keys; the last slice to finish
@@ -725,7 +734,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         // back the whole L2): the keys only ever move through device-scope
         // atomics and sc1 loads/stores, each wave drains its atomics before
         // the barrier, and the slice counter is a relaxed device atomic.
-        for (int p = tid; p < TH * TW; p += VWG) {
+        for (int p = tid; p < TH * TW; p += NT) {
             const int lx = p & (TW - 1), ly = p / TW;
             if (lx >= wlim || ly >= hlim) continue;
             u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
@@ -742,7 +751,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
         }
         __syncthreads();
         if (!sLast) continue;
-        for (int p = tid; p < TH * TW; p += VWG) {   // merged keys -> LDS, global keys back to neutral
+        for (int p = tid; p < TH * TW; p += NT) {   // merged keys -> LDS, global keys back to neutral
             const int lx = p & (TW - 1), ly = p / TW;
             if (lx >= wlim || ly >= hlim) continue;
             u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
@@ -750,7 +759,7 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
             __hip_atomic_store(g, ZMODE == 1 ? ~0ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        shade_tile<ZMODE, GOURAUD, VWG>(fp, x0, y0, wlim, hlim, key, lds, nU);
+        shade_tile<ZMODE, GOURAUD, NT>(fp, x0, y0, wlim, hlim, key, lds, nU);
     }   // work items
     if (COUNT) {
         __syncthreads();
@@ -760,18 +769,44 @@ __global__ __launch_bounds__(VWG) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVE
     }
 }
 
+// k_vis runs 2 * VWG-thread workgroups when the last batch had a few dense
+// tiles (>= HEAVY_PAIRS pairs), fewer than NR_WIDE_HEAVY (512, half the chip's
+// k_vis workgroup slots): each dense item is then latency-bound at low
+// occupancy and gains from more waves (C3 sharded 8 ways -18 %, 4 ways
+// -14 %; 2 ways +6 %, hence the threshold); with many dense tiles (C3
+// unsharded, 2 ways) or none (C2) the narrow
+// workgroups are faster.
+static u32 wide_heavy() {
+    static const u32 v = [] {
+        const char* e = getenv("NR_WIDE_HEAVY");
+        return e ? (u32)atol(e) : 512u;
+    }();
+    return v;
+}
+
 template <int Z, bool C, bool G>
 void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid, hipStream_t s) {
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
     const bool coop = sc.coopMode ? sc.coopMode == 1
                                   : (sc.lastN == 0 || sc.lastPairs > (u64)(COOP_PAIRS * (f64)sc.lastN));
-    if (coop)
-        hipLaunchKernelGGL((k_vis<Z, C, G, true>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
+    // wide workgroups when the last batch had few pairs (a sharded frame):
+    // its dense items run at low occupancy and are latency-bound
+    const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wide_heavy();
+    if (wide) {
+        if (coop)
+            hipLaunchKernelGGL((k_vis<Z, false, G, true, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, fp, F.fitems,
+                               F.flist, sc.vis, sc.fdone, F.dplan);
+        else
+            hipLaunchKernelGGL((k_vis<Z, false, G, false, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, fp, F.fitems,
+                               F.flist, sc.vis, sc.fdone, F.dplan);
+    } else if (coop) {
+        hipLaunchKernelGGL((k_vis<Z, C, G, true, VWG>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
                            sc.fdone, F.dplan);
-    else
-        hipLaunchKernelGGL((k_vis<Z, C, G, false>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
+    } else {
+        hipLaunchKernelGGL((k_vis<Z, C, G, false, VWG>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
                            sc.fdone, F.dplan);
+    }
 }
 
 template <int Z, bool G>
@@ -936,6 +971,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         // grow both and bin again (the plan kernel re-zeroed the counters)
         NR_CHECK(hipStreamSynchronize(sb));
         sc.lastPairs = F.h_plan[0];
+        sc.lastHeavy = F.h_plan[5];
         sc.lastN = (u64)src.n;
         grid = F.h_plan[1];
         if (F.h_plan[3]) break;
@@ -1027,6 +1063,7 @@ void settle(RenderContext* ctx) {
     }
     sc.lastN = (u64)pb->src.n;
     sc.lastPairs = F.h_plan[0];
+    sc.lastHeavy = F.h_plan[5];
     if (!F.h_plan[3]) {
         // overflow: the batch's later kernels did nothing; re-run it exactly
         // on the main stream, after everything queued so far
