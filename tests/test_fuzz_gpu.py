@@ -1,0 +1,146 @@
+"""Property-based parity: random frames (hypothesis) rendered by the HIP
+library and by the oracle must agree bit for bit -- f64 framebuffer, u32
+depth and the u8 frame.
+
+A frame is a random sequence of the operations the raster path serves:
+clears, transforms (cpp:386-444), colour transforms (cpp:623-641), triangle
+batches in every depth mode with flat/Gouraud, opaque/blended colours,
+degenerate and off-screen triangles (the new a-T path), and the
+reference primitives drawn between them (FillColor, DrawRect, DrawLine,
+DrawCircle, DrawVerticalGrd, cpp:682-948, 1285-1316) -- so the visibility
+raster, the ordered raster, the pending clears and their hand-offs are
+exercised in combinations no fixture lists.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+hypothesis = pytest.importorskip("hypothesis")
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+import scenes  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+_unit = st.floats(0.0, 1.0, allow_nan=False, width=64)
+
+
+@st.composite
+def triangle_op(draw):
+    n = draw(st.integers(0, 120))
+    seed = draw(st.integers(0, 2**31 - 1))
+    spread = draw(st.sampled_from([1.5, 6.0, 40.0, 300.0]))
+    gouraud = draw(st.booleans())
+    blended = draw(st.booleans())
+    test = draw(st.booleans())
+    write = draw(st.booleans())
+    return ("tri", n, seed, spread, gouraud, blended, test, write)
+
+
+@st.composite
+def prim_op(draw):
+    kind = draw(st.sampled_from(["fill", "rect", "line", "circle", "grd"]))
+    c = [draw(_unit) for _ in range(4)]
+    g = [draw(st.floats(-20.0, 140.0, allow_nan=False, width=64)) for _ in range(4)]
+    return (kind, c, g)
+
+
+@st.composite
+def state_op(draw):
+    kind = draw(st.sampled_from(["translate", "rotate", "scale", "ct", "save", "restore", "clear", "cleardepth"]))
+    v = [draw(st.floats(-3.0, 3.0, allow_nan=False, width=64)) for _ in range(4)]
+    return (kind, v)
+
+
+@st.composite
+def frame(draw):
+    W = draw(st.integers(1, 140))
+    H = draw(st.integers(1, 110))
+    alpha = draw(st.booleans())
+    ops = draw(st.lists(st.one_of(triangle_op(), prim_op(), state_op()), min_size=1, max_size=8))
+    return W, H, alpha, ops
+
+
+def _run(fac, W, H, alpha, ops):
+    ctx = fac.context(W, H, alpha)
+    ctx.set_color(0.25, 0.5, 0.75, 1.0)
+    ctx.clear_depth()
+    for op in ops:
+        k = op[0]
+        if k == "tri":
+            _, n, seed, spread, gouraud, blended, test, write = op
+            xy, z, c = scenes.triangle_soup(n, W, H, spread, seed=seed, gouraud=gouraud,
+                                            alpha=(0.1, 0.9) if blended else None, zrange=(-0.1, 1.1))
+            ctx.set_depth_state(test, write)
+            ctx.draw_triangles(xy, c, z=z, gouraud=gouraud)
+        elif k == "fill":
+            ctx.fill_color(*op[1])
+        elif k == "rect":
+            g = op[2]
+            ctx.draw_rect(g[0], g[1], g[2], g[3], *op[1])
+        elif k == "line":
+            g = op[2]
+            ctx.draw_line(g[0], g[1], g[2], g[3], 1.0 + abs(g[0]) % 7, *op[1])
+        elif k == "circle":
+            g = op[2]
+            ctx.draw_circle(g[0], g[1], abs(g[2]) % 50, *op[1])
+        elif k == "grd":
+            g, c = op[2], op[1]
+            ctx.draw_vertical_grd(g[0], g[1], g[2], g[3], c[0], c[1], c[2], c[3], c[3], c[2], c[1], c[0])
+        elif k == "translate":
+            ctx.translate(op[1][0] * 10, op[1][1] * 10)
+        elif k == "rotate":
+            ctx.rotate(op[1][0])
+        elif k == "scale":
+            ctx.scale(0.5 + abs(op[1][0]) / 3, 0.5 + abs(op[1][1]) / 3)
+        elif k == "ct":
+            ctx.set_color_transform(*[abs(v) / 3 for v in op[1]])
+        elif k == "save":
+            ctx.save_state()
+        elif k == "restore":
+            ctx.restore_state()
+        elif k == "clear":
+            ctx.set_color(*[abs(v) / 3 for v in op[1]])
+        elif k == "cleardepth":
+            ctx.clear_depth()
+    return {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer(), "u8": ctx.get_buffer_as_uint8_numpy()}
+
+
+@settings(max_examples=400, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(frame())
+def test_random_frames_match_oracle(gpu, oracle, fr):
+    W, H, alpha, ops = fr
+    g = _run(gpu, W, H, alpha, ops)
+    o = _run(oracle, W, H, alpha, ops)
+    for k in o:
+        assert scenes.bits_equal(g[k], o[k]), (k, ops, scenes.first_mismatch(g[k], o[k]))
+
+
+@st.composite
+def big_frame(draw):
+    """Multi-tile frames: thousands of triangles, split tile lists, the
+    wave-cooperative raster of large triangles and both workgroup sizes."""
+    W = draw(st.integers(64, 700))
+    H = draw(st.integers(32, 420))
+    alpha = draw(st.booleans())
+    ops = []
+    for _ in range(draw(st.integers(1, 3))):
+        op = list(draw(triangle_op()))
+        op[1] = draw(st.integers(0, 4000))
+        ops.append(tuple(op))
+        if draw(st.booleans()):
+            ops.append(draw(st.one_of(prim_op(), state_op())))
+    return W, H, alpha, ops
+
+
+@settings(max_examples=40, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(big_frame())
+def test_random_large_frames_match_oracle(gpu, oracle, fr):
+    W, H, alpha, ops = fr
+    g = _run(gpu, W, H, alpha, ops)
+    o = _run(oracle, W, H, alpha, ops)
+    for k in o:
+        assert scenes.bits_equal(g[k], o[k]), (k, ops, scenes.first_mismatch(g[k], o[k]))
