@@ -528,7 +528,7 @@ __device__ __forceinline__ f64 readlane_f64(f64 v, int lane) {
 }
 
 #ifndef NR_BIG_PX
-#define NR_BIG_PX 96
+#define NR_BIG_PX 32
 #endif
 // A triangle whose bounding box covers at least BIG_PX pixels of the tile is
 // rasterised by the whole wave rather than by its own lane.
