@@ -102,6 +102,7 @@ DEVICE_ABI = {
     "GatherFrameU8": (B, (P, P, L)),
     "GetFrameU8": (None, (P, P)),
     "GetFrameU8DevicePtr": (P, (P,)),
+    "GetFrameYUV420P": (B, (P, P)),
     "GatherFramebuffer": (B, (P, P, L)),
     "GatherFrameU8Local": (B, (P, L, L)),
     "CreateMilthmHitEffectTextures": (B, (P, D, P, L, D, D, D, P)),

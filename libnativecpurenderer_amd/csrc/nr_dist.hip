@@ -109,6 +109,29 @@ __global__ void k_to_u8_rows(const f64* __restrict__ src, iu8* __restrict__ dst,
         dst[base + i] = nr_to_u8(src[base + i]);
 }
 
+// YUV420P from the u8 frame (GetFrameYUV420P): one thread per 2x2 block.
+constexpr int YRY = 8414, YGY = 16519, YBY = 3208;      // 0.299/0.587/0.114 * 219/255 * 2^15
+constexpr int YRU = -4864, YGU = -9527, YBU = 14392;    // -0.169/-0.331/0.5 * 224/255 * 2^15
+constexpr int YRV = 14392, YGV = -12060, YBV = -2331;   // 0.5/-0.419/-0.081 * 224/255 * 2^15
+__global__ void k_yuv420p(const iu8* __restrict__ rgb, int ipp, i64 W, i64 H, iu8* __restrict__ yp,
+                          iu8* __restrict__ up, iu8* __restrict__ vp) {
+    const i64 cw = W / 2, n = cw * (H / 2);
+    for (i64 q = (i64)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (i64)gridDim.x * blockDim.x) {
+        const i64 cy = q / cw, cx = q - cy * cw;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const i64 x = 2 * cx + (k & 1), y = 2 * cy + (k >> 1);
+            const iu8* px = rgb + (y * W + x) * ipp;
+            const int r = px[0], g = px[1], b = px[2];
+            yp[y * W + x] = (iu8)(((YRY * r + YGY * g + YBY * b) >> 15) + 16);
+            if (k == 0) {
+                up[q] = (iu8)(((YRU * r + YGU * g + YBU * b) >> 15) + 128);
+                vp[q] = (iu8)(((YRV * r + YGV * g + YBV * b) >> 15) + 128);
+            }
+        }
+    }
+}
+
 constexpr int BAND = 32;   // = nrtri::TH, the tile height
 
 ShardMap shard_map(const RenderContext* ctx) {
@@ -491,6 +514,40 @@ void GetFrameU8(RenderContext* ctx, iu8* out) {
                             (size_t)(ctx->width * ctx->height * (ctx->enableAlpha ? 4 : 3)), hipMemcpyDeviceToHost,
                             ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));
+}
+
+// NEW: the frame of the last GatherFrameU8 as YUV420P planes
+// (Y W*H, then U and V (W/2)*(H/2) each, W and H even), the encoder input of
+// PutRendererContextFrame (cpp:232-275, sws_scale RGB24/RGBA -> YUV420P).
+// Converted on the GPU so the host receives 1.5 bytes per pixel instead of
+// 3 or 4.  Arithmetic: swscale's unscaled RGB -> YV12 converter (rgb2rgb's
+// rgb24toyv12): BT.601 limited range, 15-bit fixed-point coefficients
+// (0.299/0.587/0.114 x 219/255, chroma x 224/255, rounded), Y/U/V =
+// (c . rgb >> 15) + 16/128/128, chroma point-sampled at the even pixel of each
+// 2x2 block.  Parity unpinned: FFmpeg is absent here, and which of swscale's
+// converters a given FFmpeg build picks (this one or the bilinear scaler path)
+// depends on its version.  Returns false for odd sizes.
+bool GetFrameYUV420P(RenderContext* ctx, iu8* out) {
+    NR_CHECK(hipSetDevice(ctx->device));
+    const i64 W = ctx->width, H = ctx->height;
+    if ((W & 1) || (H & 1)) {
+        nr_set_error_msg("GetFrameYUV420P: width and height must be even");
+        return false;
+    }
+    if (ctx->frameLast < 0 || !ctx->frameBuf[ctx->frameLast] || W * H == 0) return W * H == 0;
+    if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
+    const size_t bytes = (size_t)(W * H + 2 * (W / 2) * (H / 2));
+    iu8* d = nullptr;
+    NR_CHECK(hipMallocAsync((void**)&d, bytes, ctx->stream));
+    const i64 blocks = (W / 2) * (H / 2);
+    hipLaunchKernelGGL(k_yuv420p, dim3((unsigned)std::min<i64>((blocks + 255) / 256, 16384)), dim3(256), 0,
+                       ctx->stream, ctx->frameBuf[ctx->frameLast], ctx->enableAlpha ? 4 : 3, W, H, d, d + W * H,
+                       d + W * H + blocks);
+    NR_CHECK(hipGetLastError());
+    NR_CHECK(hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    NR_CHECK(hipFreeAsync(d, ctx->stream));
+    NR_CHECK(hipStreamSynchronize(ctx->stream));
+    return true;
 }
 
 // NEW: device pointer of that frame (complete once Flush returns).

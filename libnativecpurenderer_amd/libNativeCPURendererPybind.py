@@ -354,6 +354,15 @@ class RenderContext:
         if not lib.GatherFrameU8Local(arr, len(ctxs), root):
             raise RuntimeError("GatherFrameU8Local failed: " + _lib.last_error())
 
+    def get_frame_yuv420p(self) -> np.ndarray:
+        """YUV420P planes (Y, then U, then V) of the last gathered frame,
+        converted on the GPU (GetFrameYUV420P; W and H even)."""
+        n = self.width * self.height + 2 * (self.width // 2) * (self.height // 2)
+        out = np.empty(n, dtype=np.uint8)
+        if not lib.GetFrameYUV420P(self._ptr, out.ctypes.data_as(ctypes.c_void_p)):
+            raise RuntimeError("GetFrameYUV420P failed: " + _lib.last_error())
+        return out
+
     def gather_framebuffer(self, comm: "Comm", root: int = 0):
         """f64 framebuffer (+ depth) bands of every rank assembled on `root`."""
         if not lib.GatherFramebuffer(self._ptr, comm._ptr, root):

@@ -649,3 +649,24 @@ def oracle_hit_effect(mask_u8, seed, t, rgb=(0x96 / 0xff, 0x90 / 0xff, 0xfd / 0x
     lib.DestroyTexture(tex)
     lib.DestroyTexture(m)
     return out
+
+
+# ---------------------------------------------------------------------------
+# YUV420P restatement (GetFrameYUV420P; swscale's unscaled rgb24toyv12 path)
+# ---------------------------------------------------------------------------
+YUV_COEF = ((8414, 16519, 3208), (-4864, -9527, 14392), (14392, -12060, -2331))
+
+
+def yuv420p(rgb_u8):
+    """(H, W, 3|4) u8 frame -> flat Y | U | V planes: BT.601 limited range,
+    15-bit coefficients, (c . rgb >> 15) + 16/128/128 (arithmetic shift),
+    chroma taken at the top-left pixel of each 2x2 block."""
+    h, w = rgb_u8.shape[:2]
+    p = rgb_u8[..., :3].astype(np.int64)
+    r, g, b = p[..., 0], p[..., 1], p[..., 2]
+    (ry, gy, by), (ru, gu, bu), (rv, gv, bv) = YUV_COEF
+    y = ((ry * r + gy * g + by * b) >> 15) + 16
+    rs, gs, bs = r[0::2, 0::2], g[0::2, 0::2], b[0::2, 0::2]
+    u = ((ru * rs + gu * gs + bu * bs) >> 15) + 128
+    v = ((rv * rs + gv * gs + bv * bs) >> 15) + 128
+    return np.concatenate([y.ravel(), u.ravel(), v.ravel()]).astype(np.uint8)

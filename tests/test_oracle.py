@@ -397,3 +397,15 @@ def test_oracle_hit_effect_needs_alpha():
     rgb = np.zeros((4, 4, 3), dtype=np.uint8)
     m = lib.CreateTextureUInt8(4, 4, False, rgb.ctypes.data_as(scenes.ctypes.c_void_p))
     assert not lib.CreateMilthmHitEffectTexture(m, 0.1, 0.5, 1.0, 1.0, 1.0)   # NULL (cpp:1418)
+
+
+def test_yuv420p_restatement_known_values():
+    """BT.601 limited range with this converter's truncating shift: black ->
+    (16, 128, 128); white -> (234, 128, 128) and pure red -> (81, 90, 239),
+    one below the nominal 235 / 240 where the product sum is just under the
+    next integer (the fast path truncates instead of rounding)."""
+    for rgb, want in (((0, 0, 0), (16, 128, 128)), ((255, 255, 255), (234, 128, 128)), ((255, 0, 0), (81, 90, 239))):
+        img = np.zeros((2, 2, 3), dtype=np.uint8)
+        img[...] = rgb
+        out = scenes.yuv420p(img)
+        assert tuple(int(v) for v in (out[0], out[4], out[5])) == want

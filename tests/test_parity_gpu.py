@@ -459,3 +459,31 @@ def test_bench_multi_rank_orchestration_on_one_gpu(gpu, tmp_path):
     d = json.loads(line)
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 5
     assert set(d["config"]["partition_calibration_ms"]) >= {"equal", "3", "12"}
+
+
+@pytest.mark.parametrize("alpha", [False, True])
+def test_frame_yuv420p_matches_restatement(gpu, alpha):
+    """GetFrameYUV420P (§8f-2) converts the gathered u8 frame on the GPU:
+    equal, byte for byte, to the numpy restatement applied to the same frame
+    (and to the oracle's u8 image of the same scene)."""
+    W, H = 322, 190
+    xy, z, c = scenes.triangle_soup(1500, W, H, 25, seed=5, gouraud=True)
+    outs = {}
+    for fac in (gpu, scenes.OracleFactory()):
+        ctx = fac.context(W, H, alpha)
+        ctx.set_color(0.1, 0.6, 0.3, 1.0)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.draw_triangles(xy, c, z=z)
+        ctx.draw_rect(10, 10, 100, 60, 1.0, 0.2, 0.1, 0.5)
+        outs[fac.name] = ctx
+    g = outs["gpu"]
+    g.gather_frame_u8()
+    got = g.get_frame_yuv420p()
+    want = scenes.yuv420p(outs["oracle"].get_buffer_as_uint8_numpy())
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    assert np.array_equal(scenes.yuv420p(g.get_frame_u8()), want)
+    odd = gpu.context(5, 4, False)
+    odd.gather_frame_u8()
+    with pytest.raises(RuntimeError):
+        odd.get_frame_yuv420p()
