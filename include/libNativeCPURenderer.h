@@ -54,6 +54,40 @@ i64 GetTextureWidth(Texture* tex);                                       /* h:12
 i64 GetTextureHeight(Texture* tex);                                      /* h:121 */
 bool GetTextureEnableAlpha(Texture* tex);                                /* h:122 */
 
+/* ---- audio clips (cpp:990-1283): interleaved f64 samples in HBM, ops as kernels */
+typedef struct AudioClip AudioClip;           /* h:70-75 (opaque here) */
+typedef struct WapperedBytes WapperedBytes;   /* h:77-80 (opaque here) */
+i64 GetAudioClipBufferSizeFromData(i64 numFrames, i64 channels);          /* h:123 */
+i64 GetAudioClipBufferSize(AudioClip* clip);                              /* h:124 */
+AudioClip* CreateAudioClipFromBuffer(i64 sampleRate, i64 channels, i64 numFrames, f64* buffer); /* h:125 */
+AudioClip* CreateAudioClipFromInt16Buffer(i64 sampleRate, i64 channels, i64 numFrames, short* buffer); /* h:126 */
+AudioClip* CreateSilentAudioClip(i64 sampleRate, i64 channels, i64 numFrames); /* h:127 */
+void DestroyAudioClip(AudioClip* clip);                                   /* h:128 (frees; a no-op there) */
+AudioClip* CloneAudioClip(AudioClip* clip);                               /* h:129 */
+void ApplyResampleAudioClip(AudioClip* clip, i64 sampleRate, i64 channels); /* h:130 */
+void ResampleAudioClipLike(AudioClip* clip, AudioClip* like);             /* h:131 */
+i64 OverlayAudioClip(AudioClip* target, AudioClip* source, i64 startFrame, bool autoResample); /* h:132;
+                                                   0, -1 rate mismatch, -2 channel mismatch, -3 devices differ */
+i64 OverlayAudioClipSecond(AudioClip* target, AudioClip* source, f64 startSecond, bool autoResample); /* h:133 */
+WapperedBytes* SaveAudioClipAsWav(AudioClip* clip);                       /* h:134 */
+i64 GetAudioClipSampleRate(AudioClip* clip);                              /* h:135 */
+i64 GetAudioClipChannels(AudioClip* clip);                                /* h:136 */
+i64 GetAudioClipNumFrames(AudioClip* clip);                               /* h:137 */
+f64 GetAudioClipDuration(AudioClip* clip);                                /* h:138 */
+iu8* GetWapperedBytesDataPtr(WapperedBytes* bytes);                       /* h:139 */
+i64 GetWapperedBytesDataSize(WapperedBytes* bytes);                       /* h:140 */
+void ApplyVolumeGain(AudioClip* clip, f64 gain);                          /* h:141 */
+void ApplyCutAudioClip(AudioClip* clip, i64 startFrame, i64 endFrame);    /* h:144 */
+void ApplySpeedAudioClip(AudioClip* clip, f64 speed);                     /* h:145 */
+i64 OverlayAudioClipMany(AudioClip* target, AudioClip* source, const i64* startFrames, i64 n,
+                         bool autoResample);  /* NEW: n OverlayAudioClip calls in order, one launch
+                                                 (the note loop of milrenderer.py:810-815) */
+i64 OverlayAudioClipManySecond(AudioClip* target, AudioClip* source, const f64* startSeconds, i64 n,
+                               bool autoResample);  /* NEW: the same with OverlayAudioClipSecond times */
+void DestroyWapperedBytes(WapperedBytes* bytes); /* NEW (the reference never frees them) */
+void GetAudioClipBuffer(AudioClip* clip, f64* out); /* NEW: samples to the host */
+void* GetAudioClipDevicePtr(AudioClip* clip);    /* NEW: samples in HBM (interop) */
+
 /* ---- texture preparation: procedural hit-effect shader (cpp:1318-1440) */
 Texture* CreateMilthmHitEffectTexture(Texture* mask, f64 seed, f64 t, f64 r, f64 g, f64 b); /* h:151; NULL
                                                                    when the mask has no alpha (cpp:1418) */

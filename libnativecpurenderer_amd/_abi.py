@@ -117,8 +117,42 @@ DEVICE_ABI = {
     "IsRecordingCommands": (B, (P,)),
 }
 
-HIP_LIBRARY_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **DEVICE_ABI}
-ORACLE_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, "OracleLastFragmentCount": (L, ()),
+# Audio clips (h:123-145).  OverlayAudioClip's startFrame is an
+# i64 here: the reference binding declares c_double for it (Pybind:577), which
+# lands the bool in the i64 register (the frame-unit overlay is broken there).
+AUDIO_ABI = {
+    "GetAudioClipBufferSizeFromData": (L, (L, L)),
+    "GetAudioClipBufferSize": (L, (P,)),
+    "CreateAudioClipFromBuffer": (P, (L, L, L, P)),
+    "CreateAudioClipFromInt16Buffer": (P, (L, L, L, P)),
+    "CreateSilentAudioClip": (P, (L, L, L)),
+    "DestroyAudioClip": (None, (P,)),
+    "CloneAudioClip": (P, (P,)),
+    "ApplyResampleAudioClip": (None, (P, L, L)),
+    "ResampleAudioClipLike": (None, (P, P)),
+    "OverlayAudioClip": (L, (P, P, L, B)),
+    "OverlayAudioClipSecond": (L, (P, P, D, B)),
+    "SaveAudioClipAsWav": (P, (P,)),
+    "GetAudioClipSampleRate": (L, (P,)),
+    "GetAudioClipChannels": (L, (P,)),
+    "GetAudioClipNumFrames": (L, (P,)),
+    "GetAudioClipDuration": (D, (P,)),
+    "GetWapperedBytesDataPtr": (P, (P,)),
+    "GetWapperedBytesDataSize": (L, (P,)),
+    "DestroyWapperedBytes": (None, (P,)),
+    "ApplyVolumeGain": (None, (P, D)),
+    "ApplyCutAudioClip": (None, (P, L, L)),
+    "ApplySpeedAudioClip": (None, (P, D)),
+    "GetAudioClipBuffer": (None, (P, P)),
+}
+AUDIO_DEVICE_ABI = {
+    "OverlayAudioClipMany": (L, (P, P, P, L, B)),
+    "OverlayAudioClipManySecond": (L, (P, P, P, L, B)),
+    "GetAudioClipDevicePtr": (P, (P,)),
+}
+
+HIP_LIBRARY_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **DEVICE_ABI, **AUDIO_ABI, **AUDIO_DEVICE_ABI}
+ORACLE_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **AUDIO_ABI, "OracleLastFragmentCount": (L, ()),
               "OracleGetTextureBuffer": (None, (P, P))}
 
 

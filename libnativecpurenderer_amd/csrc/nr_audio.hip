@@ -1,0 +1,457 @@
+// nr_audio.hip — audio clips: the sample buffers of
+// milrenderer's hit-sound mix (milrenderer.py:803-815, hjm_mixer.py:67-97)
+// kept in HBM, and the reference's clip operations (cpp:990-1283) as kernels.
+//
+// Layout: the reference's interleaved f64 samples, `buffer[frame * channels
+// + c]` (cpp:1007-1011), so a clip's readback and its WAV export are one copy.
+// Every per-sample expression is the reference's, in its order, in f64 with
+// no FMA (-ffp-contract=off), so results are bit-identical.
+//
+// The mix is the hot part: thousands of OverlayAudioClip calls, each adding a
+// short clip into the song at a note time.  Sequential f64 adds do not
+// commute, so OverlayAudioClipMany (new) keeps the call order per sample: a
+// workgroup owns 256 consecutive samples of the target, finds the overlays
+// touching them 256 starts at a time (ballot + prefix count into LDS, in call
+// order) and each thread adds its sample's contributions in that order —
+// identical to n calls of OverlayAudioClip, in one launch.
+//
+// Where the reference reads or writes outside a buffer (undefined behaviour)
+// this library defines the result, and the oracle does the same:
+//  * OverlayAudioClip with startFrame < 0: frames landing before the target
+//    are skipped (the reference writes before the buffer);
+//  * ApplyResampleAudioClip reads index `numFrames - channels - 1` at most
+//    (cpp:1081-1084, the frame count compared with the channel count): a
+//    negative index (clips of <= channels frames) reads 0.0;
+//  * ApplyCutAudioClip leaves frames past the source uninitialised
+//    (cpp:1265-1279): they are 0.0 here, as are frames before a negative start;
+//    a negative length gives an empty clip (the reference's `new f64[n < 0]`
+//    throws);
+//  * a negative resampled length gives an empty clip.
+#include "nr_common.h"
+
+#include <cstring>
+
+struct AudioClip {   // h:70-75, samples in HBM
+    i64 sampleRate;
+    i64 channels;
+    i64 numFrames;
+    f64* buffer;     // device, numFrames * channels (at least one element allocated)
+    int device;
+};
+
+struct WapperedBytes {   // h:77-80, host bytes
+    iu8* data;
+    i64 size;
+};
+
+namespace {
+
+constexpr int AWG = 256;
+
+int grid_for(i64 n) {
+    i64 g = (n + AWG - 1) / AWG;
+    if (g < 1) g = 1;
+    if (g > 65535) g = 65535;
+    return (int)g;
+}
+
+// Plain hipMalloc/hipFree (hipFree waits for the device), not the stream-
+// ordered allocator: a mix run with hipMallocAsync/hipFreeAsync buffers once
+// read back a stale 32 MiB span of a clip (not reproduced since); the clip
+// operations are not latency-bound, so the simpler allocator is kept.
+f64* alloc_samples(i64 n, hipStream_t) {
+    f64* p = nullptr;
+    NR_CHECK(hipMalloc((void**)&p, (size_t)(n > 0 ? n : 1) * sizeof(f64)));
+    return p;
+}
+
+// cpp:1029: (f64)v / 32768.0
+__global__ void k_i16_to_f64(const short* __restrict__ in, f64* __restrict__ out, i64 n) {
+    for (i64 i = (i64)blockIdx.x * AWG + threadIdx.x; i < n; i += (i64)gridDim.x * AWG) out[i] = (f64)in[i] / 32768.0;
+}
+
+// cpp:1254-1259
+__global__ void k_gain(f64* __restrict__ p, i64 n, f64 gain) {
+    for (i64 i = (i64)blockIdx.x * AWG + threadIdx.x; i < n; i += (i64)gridDim.x * AWG) p[i] *= gain;
+}
+
+__device__ __forceinline__ f64 sample_at(const f64* b, i64 idx) { return idx >= 0 ? b[idx] : 0.0; }
+
+// cpp:1063-1120, one thread per new frame
+__global__ void k_resample(const f64* __restrict__ src, i64 oldFrames, i64 oldCh, i64 oldRate, f64* __restrict__ dst,
+                           i64 newFrames, i64 newCh, i64 newRate) {
+    for (i64 i = (i64)blockIdx.x * AWG + threadIdx.x; i < newFrames; i += (i64)gridDim.x * AWG) {
+        const f64 secT = (f64)i / (f64)newRate;
+        const f64 old = secT * (f64)oldRate;
+        i64 fl = (i64)floor(old), ce = (i64)ceil(old);
+        const i64 lim = oldFrames - oldCh;
+        if (fl < 0) fl = 0;
+        if (fl >= lim) fl = lim - 1;
+        if (ce < 0) ce = 0;
+        if (ce >= lim) ce = lim - 1;
+        const f64 frac = old - (f64)fl;
+        if (oldCh == newCh) {
+            for (i64 c = 0; c < newCh; ++c) {
+                const f64 vf = sample_at(src, fl * oldCh + c), vc = sample_at(src, ce * oldCh + c);
+                dst[i * newCh + c] = vf + (vc - vf) * frac;
+            }
+        } else {
+            f64 sf = 0, sc = 0;
+            for (i64 c = 0; c < oldCh; ++c) {
+                sf += sample_at(src, fl * oldCh + c);
+                sc += sample_at(src, ce * oldCh + c);
+            }
+            const f64 dc = (f64)oldCh;
+            const f64 v = sf / dc + (sc / dc - sf / dc) * frac;
+            for (i64 c = 0; c < newCh; ++c) dst[i * newCh + c] = v;
+        }
+    }
+}
+
+// cpp:1145-1151, one thread per source sample
+__global__ void k_overlay(f64* __restrict__ tgt, i64 tgtFrames, const f64* __restrict__ src, i64 srcFrames, i64 ch,
+                          i64 start) {
+    const i64 n = srcFrames * ch;
+    for (i64 e = (i64)blockIdx.x * AWG + threadIdx.x; e < n; e += (i64)gridDim.x * AWG) {
+        const i64 i = e / ch, c = e - i * ch;
+        const i64 t = start + i;
+        if (t < 0 || t >= tgtFrames) continue;
+        tgt[t * ch + c] += src[e];
+    }
+}
+
+// n overlays of one source in call order (see the file comment).  Workgroup =
+// 256 consecutive target samples.
+__global__ __launch_bounds__(AWG) void k_overlay_many(f64* __restrict__ tgt, i64 tgtFrames, const f64* __restrict__ src,
+                                                      i64 srcFrames, i64 ch, const i64* __restrict__ starts, i64 n) {
+    __shared__ i64 hit[AWG];
+    __shared__ int wcnt[AWG / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const i64 total = tgtFrames * ch;
+    for (i64 e0 = (i64)blockIdx.x * AWG; e0 < total; e0 += (i64)gridDim.x * AWG) {
+        const i64 e = e0 + tid;
+        const bool live = e < total;
+        const i64 f = live ? e / ch : 0, c = live ? e - f * ch : 0;
+        const i64 fa = e0 / ch, fb = (min(e0 + AWG, total) - 1) / ch;   // frames this workgroup touches
+        f64 acc = live ? tgt[e] : 0.0;
+        for (i64 k0 = 0; k0 < n; k0 += AWG) {
+            const i64 k = k0 + tid;
+            bool h = false;
+            i64 s = 0;
+            if (k < n) {
+                s = starts[k];
+                h = s <= fb && s > fa - srcFrames;
+            }
+            const u64 m = __ballot(h);
+            if (lane == 0) wcnt[w] = __popcll(m);
+            __syncthreads();
+            int base = 0, cnt = 0;
+#pragma unroll
+            for (int q = 0; q < AWG / 64; ++q) {
+                base += q < w ? wcnt[q] : 0;
+                cnt += wcnt[q];
+            }
+            if (h) hit[base + __popcll(m & ((1ull << lane) - 1ull))] = s;
+            __syncthreads();
+            if (live)
+                for (int q = 0; q < cnt; ++q) {
+                    const i64 i = f - hit[q];
+                    if (i >= 0 && i < srcFrames) acc += src[i * ch + c];
+                }
+            __syncthreads();
+        }
+        if (live) tgt[e] = acc;
+    }
+}
+
+// cpp:1265-1279 (see the file comment for frames outside the source)
+__global__ void k_cut(const f64* __restrict__ src, i64 srcFrames, i64 ch, i64 start, f64* __restrict__ dst, i64 frames) {
+    const i64 n = frames * ch;
+    for (i64 e = (i64)blockIdx.x * AWG + threadIdx.x; e < n; e += (i64)gridDim.x * AWG) {
+        const i64 i = e / ch, c = e - i * ch;
+        const i64 sf = start + i;
+        dst[e] = (sf >= 0 && sf < srcFrames) ? src[sf * ch + c] : 0.0;
+    }
+}
+
+// cpp:1215-1222: (i16)(clamp(v, -1, 1) * 32767.0); the x86 conversion goes
+// through int32, and a NaN (which passes the clamp) becomes 0x80000000 -> 0.
+__global__ void k_to_i16(const f64* __restrict__ p, short* __restrict__ out, i64 n) {
+    for (i64 i = (i64)blockIdx.x * AWG + threadIdx.x; i < n; i += (i64)gridDim.x * AWG) {
+        const f64 v = p[i];
+        const f64 x = (v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v)) * 32767.0;
+        out[i] = x != x ? (short)0 : (short)(int)x;
+    }
+}
+
+AudioClip* new_clip(i64 rate, i64 ch, i64 frames) {
+    AudioClip* a = new AudioClip();
+    a->sampleRate = rate; a->channels = ch; a->numFrames = frames;
+    NR_CHECK(hipGetDevice(&a->device));
+    a->buffer = alloc_samples(frames * ch, nr_stream_for(a->device));
+    return a;
+}
+
+// frees a buffer the stream may still be using
+void free_after(hipStream_t s, void* p) {
+    NR_CHECK(hipStreamSynchronize(s));
+    NR_CHECK(hipFree(p));
+}
+
+hipStream_t clip_stream(AudioClip* a) {
+    NR_CHECK(hipSetDevice(a->device));
+    return nr_stream_for(a->device);
+}
+
+}  // namespace
+
+extern "C" {
+
+// cpp:990-996
+i64 GetAudioClipBufferSizeFromData(i64 numFrames, i64 channels) { return numFrames * channels; }
+i64 GetAudioClipBufferSize(AudioClip* clip) { return clip->numFrames * clip->channels; }
+
+// cpp:998-1012 (the caller's samples are copied)
+AudioClip* CreateAudioClipFromBuffer(i64 sampleRate, i64 channels, i64 numFrames, f64* buffer) {
+    AudioClip* a = new_clip(sampleRate, channels, numFrames);
+    hipStream_t s = nr_stream_for(a->device);
+    const i64 n = numFrames * channels;
+    if (n > 0) NR_CHECK(hipMemcpyAsync(a->buffer, buffer, (size_t)n * sizeof(f64), hipMemcpyHostToDevice, s));
+    NR_CHECK(hipStreamSynchronize(s));   // caller owns `buffer`
+    return a;
+}
+
+// cpp:1016-1034: i16 -> f64 on the GPU
+AudioClip* CreateAudioClipFromInt16Buffer(i64 sampleRate, i64 channels, i64 numFrames, short* buffer) {
+    AudioClip* a = new_clip(sampleRate, channels, numFrames);
+    hipStream_t s = nr_stream_for(a->device);
+    const i64 n = numFrames * channels;
+    if (n > 0) {
+        short* d = nullptr;
+        NR_CHECK(hipMalloc((void**)&d, (size_t)n * sizeof(short)));
+        NR_CHECK(hipMemcpyAsync(d, buffer, (size_t)n * sizeof(short), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_i16_to_f64, dim3(grid_for(n)), dim3(AWG), 0, s, d, a->buffer, n);
+        NR_CHECK(hipGetLastError());
+        free_after(s, d);
+    }
+    NR_CHECK(hipStreamSynchronize(s));
+    return a;
+}
+
+// cpp:1036-1046
+AudioClip* CreateSilentAudioClip(i64 sampleRate, i64 channels, i64 numFrames) {
+    AudioClip* a = new_clip(sampleRate, channels, numFrames);
+    const i64 n = numFrames * channels;
+    if (n > 0) NR_CHECK(hipMemsetAsync(a->buffer, 0, (size_t)n * sizeof(f64), nr_stream_for(a->device)));
+    return a;
+}
+
+// cpp:1048-1052 is a no-op (the reference leaks); here the clip is freed
+void DestroyAudioClip(AudioClip* clip) {
+    if (!clip) return;
+    hipStream_t s = clip_stream(clip);
+    free_after(s, clip->buffer);
+    delete clip;
+}
+
+// cpp:1054-1061
+AudioClip* CloneAudioClip(AudioClip* clip) {
+    hipStream_t s = clip_stream(clip);
+    AudioClip* a = new_clip(clip->sampleRate, clip->channels, clip->numFrames);
+    const i64 n = clip->numFrames * clip->channels;
+    if (n > 0) NR_CHECK(hipMemcpyAsync(a->buffer, clip->buffer, (size_t)n * sizeof(f64), hipMemcpyDeviceToDevice, s));
+    return a;
+}
+
+// cpp:1242-1244
+f64 GetAudioClipDuration(AudioClip* clip) { return (f64)clip->numFrames / (f64)clip->sampleRate; }
+
+// cpp:1063-1120
+void ApplyResampleAudioClip(AudioClip* clip, i64 sampleRate, i64 channels) {
+    if (clip->sampleRate == sampleRate && clip->channels == channels) return;
+    const f64 dur = GetAudioClipDuration(clip);
+    i64 frames = nr_f2i64(dur * (f64)sampleRate);
+    if (frames < 0) frames = 0;
+    hipStream_t s = clip_stream(clip);
+    f64* nb = alloc_samples(frames * channels, s);
+    if (frames > 0 && channels > 0) {
+        hipLaunchKernelGGL(k_resample, dim3(grid_for(frames)), dim3(AWG), 0, s, clip->buffer, clip->numFrames,
+                           clip->channels, clip->sampleRate, nb, frames, channels, sampleRate);
+        NR_CHECK(hipGetLastError());
+    }
+    free_after(s, clip->buffer);
+    clip->buffer = nb;
+    clip->sampleRate = sampleRate;
+    clip->channels = channels;
+    clip->numFrames = frames;
+}
+
+// cpp:1122-1127
+void ResampleAudioClipLike(AudioClip* clip, AudioClip* like) {
+    ApplyResampleAudioClip(clip, like->sampleRate, like->channels);
+}
+
+// Shared front half of OverlayAudioClip(Many), cpp:1135-1143: the resampled
+// copy of `source` when asked for and needed (released by the caller; the
+// reference leaks it), or an error code.
+static i64 overlay_source(AudioClip* target, AudioClip*& source, bool autoResample, AudioClip*& tmp) {
+    tmp = nullptr;
+    if (target->device != source->device) {
+        nr_set_error_msg("OverlayAudioClip: target and source live on different devices");
+        return -3;
+    }
+    if (autoResample && (target->sampleRate != source->sampleRate || target->channels != source->channels)) {
+        tmp = CloneAudioClip(source);
+        ResampleAudioClipLike(tmp, target);
+        source = tmp;
+    }
+    if (target->sampleRate != source->sampleRate) return -1;
+    if (target->channels != source->channels) return -2;
+    return 0;
+}
+
+// cpp:1129-1154
+i64 OverlayAudioClip(AudioClip* target, AudioClip* source, i64 startFrame, bool autoResample) {
+    AudioClip* tmp;
+    const i64 rc = overlay_source(target, source, autoResample, tmp);
+    if (rc == 0) {
+        hipStream_t s = clip_stream(target);
+        const i64 n = source->numFrames * source->channels;
+        if (n > 0 && startFrame < target->numFrames) {
+            hipLaunchKernelGGL(k_overlay, dim3(grid_for(n)), dim3(AWG), 0, s, target->buffer, target->numFrames,
+                               source->buffer, source->numFrames, source->channels, startFrame);
+            NR_CHECK(hipGetLastError());
+        }
+    }
+    if (tmp) DestroyAudioClip(tmp);
+    return rc;
+}
+
+// cpp:1156-1163
+i64 OverlayAudioClipSecond(AudioClip* target, AudioClip* source, f64 startSecond, bool autoResample) {
+    return OverlayAudioClip(target, source, nr_f2i64(startSecond * (f64)target->sampleRate), autoResample);
+}
+
+// NEW: n calls of OverlayAudioClip(target, source, startFrames[k], autoResample)
+// in order, as one launch (the note loop of milrenderer.py:810-815).  Same
+// return codes; the source is resampled at most once.
+i64 OverlayAudioClipMany(AudioClip* target, AudioClip* source, const i64* startFrames, i64 n, bool autoResample) {
+    AudioClip* tmp;
+    const i64 rc = overlay_source(target, source, autoResample, tmp);
+    const i64 total = target->numFrames * target->channels;
+    if (rc == 0 && n > 0 && total > 0 && source->numFrames > 0) {
+        hipStream_t s = clip_stream(target);
+        i64* d = nullptr;
+        NR_CHECK(hipMalloc((void**)&d, (size_t)n * sizeof(i64)));
+        NR_CHECK(hipMemcpyAsync(d, startFrames, (size_t)n * sizeof(i64), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_overlay_many, dim3(grid_for(total)), dim3(AWG), 0, s, target->buffer, target->numFrames,
+                           source->buffer, source->numFrames, source->channels, d, n);
+        NR_CHECK(hipGetLastError());
+        free_after(s, d);
+        NR_CHECK(hipStreamSynchronize(s));   // caller owns startFrames
+    }
+    if (tmp) DestroyAudioClip(tmp);
+    return rc;
+}
+
+// NEW: OverlayAudioClipMany with start times in seconds (cpp:1162 per time)
+i64 OverlayAudioClipManySecond(AudioClip* target, AudioClip* source, const f64* startSeconds, i64 n,
+                               bool autoResample) {
+    std::vector<i64> f((size_t)(n > 0 ? n : 0));
+    for (i64 k = 0; k < n; ++k) f[(size_t)k] = nr_f2i64(startSeconds[k] * (f64)target->sampleRate);
+    return OverlayAudioClipMany(target, source, f.data(), n, autoResample);
+}
+
+// cpp:1165-1228: RIFF/WAVE PCM16 header built on the host, samples converted
+// on the GPU and copied behind it
+WapperedBytes* SaveAudioClipAsWav(AudioClip* clip) {
+    const i64 n = clip->numFrames * clip->channels;
+    const i64 size = 44 + n * 2;
+    WapperedBytes* w = new WapperedBytes();
+    w->size = size;
+    w->data = new iu8[(size_t)size];
+    iu8* d = w->data;
+    auto put32 = [&](int off, int32_t v) { std::memcpy(d + off, &v, 4); };
+    auto put16 = [&](int off, int16_t v) { std::memcpy(d + off, &v, 2); };
+    std::memcpy(d + 0, "RIFF", 4);
+    put32(4, (int32_t)(size - 8));
+    std::memcpy(d + 8, "WAVEfmt ", 8);
+    put32(16, 0x10);
+    put16(20, 1);
+    put16(22, (int16_t)clip->channels);
+    put32(24, (int32_t)clip->sampleRate);
+    put32(28, (int32_t)(clip->sampleRate * clip->channels * 2));
+    put16(32, (int16_t)(clip->channels * 2));
+    put16(34, 16);
+    std::memcpy(d + 36, "data", 4);
+    put32(40, (int32_t)(n * 2));
+    hipStream_t s = clip_stream(clip);
+    if (n > 0) {
+        short* dv = nullptr;
+        NR_CHECK(hipMalloc((void**)&dv, (size_t)n * sizeof(short)));
+        hipLaunchKernelGGL(k_to_i16, dim3(grid_for(n)), dim3(AWG), 0, s, clip->buffer, dv, n);
+        NR_CHECK(hipGetLastError());
+        NR_CHECK(hipMemcpyAsync(d + 44, dv, (size_t)n * sizeof(short), hipMemcpyDeviceToHost, s));
+        free_after(s, dv);
+    }
+    NR_CHECK(hipStreamSynchronize(s));
+    return w;
+}
+
+i64 GetAudioClipSampleRate(AudioClip* clip) { return clip->sampleRate; }   // cpp:1230-1232
+i64 GetAudioClipChannels(AudioClip* clip) { return clip->channels; }       // cpp:1234-1236
+i64 GetAudioClipNumFrames(AudioClip* clip) { return clip->numFrames; }     // cpp:1238-1240
+iu8* GetWapperedBytesDataPtr(WapperedBytes* bytes) { return bytes->data; } // cpp:1246-1248
+i64 GetWapperedBytesDataSize(WapperedBytes* bytes) { return bytes->size; } // cpp:1250-1252
+
+// NEW: the reference never frees WapperedBytes
+void DestroyWapperedBytes(WapperedBytes* bytes) {
+    if (!bytes) return;
+    delete[] bytes->data;
+    delete bytes;
+}
+
+// cpp:1254-1259
+void ApplyVolumeGain(AudioClip* clip, f64 gain) {
+    const i64 n = clip->numFrames * clip->channels;
+    if (n <= 0) return;
+    hipStream_t s = clip_stream(clip);
+    hipLaunchKernelGGL(k_gain, dim3(grid_for(n)), dim3(AWG), 0, s, clip->buffer, n, gain);
+    NR_CHECK(hipGetLastError());
+}
+
+// cpp:1265-1279
+void ApplyCutAudioClip(AudioClip* clip, i64 startFrame, i64 endFrame) {
+    i64 frames = endFrame - startFrame;
+    if (frames < 0) frames = 0;
+    hipStream_t s = clip_stream(clip);
+    const i64 n = frames * clip->channels;
+    f64* nb = alloc_samples(n, s);
+    if (n > 0) {
+        hipLaunchKernelGGL(k_cut, dim3(grid_for(n)), dim3(AWG), 0, s, clip->buffer, clip->numFrames, clip->channels,
+                           startFrame, nb, frames);
+        NR_CHECK(hipGetLastError());
+    }
+    free_after(s, clip->buffer);
+    clip->buffer = nb;
+    clip->numFrames = frames;
+}
+
+// cpp:1281-1283: i64 *= f64 -> (i64)((f64)rate * speed)
+void ApplySpeedAudioClip(AudioClip* clip, f64 speed) {
+    clip->sampleRate = nr_f2i64((f64)clip->sampleRate * speed);
+}
+
+// NEW: the clip's interleaved samples into a host buffer of
+// GetAudioClipBufferSize(clip) doubles
+void GetAudioClipBuffer(AudioClip* clip, f64* out) {
+    const i64 n = clip->numFrames * clip->channels;
+    hipStream_t s = clip_stream(clip);
+    if (n > 0) NR_CHECK(hipMemcpyAsync(out, clip->buffer, (size_t)n * sizeof(f64), hipMemcpyDeviceToHost, s));
+    NR_CHECK(hipStreamSynchronize(s));
+}
+
+// NEW: the device pointer of the samples (interop)
+void* GetAudioClipDevicePtr(AudioClip* clip) { return clip->buffer; }
+
+}  // extern "C"

@@ -15,9 +15,13 @@ Deliberate differences from the reference binding, each a reference bug:
     f64 parameters of GetColor, h:113, and crashes — SURVEY §8b);
   * Texture(..., is_uint8=False) works (the reference's
     `c_double * len(data) // 8` precedence bug raises TypeError, :391);
-  * apply_pixel works (the reference .so does not export ApplyPixel).
-Out of scope here (media back-ends): VideoCap, AudioClip,
-the milthm hit-effect shader and WapperedBytes helpers.
+  * apply_pixel works (the reference .so does not export ApplyPixel);
+  * AudioClip.overlay(..., time_unit="frame") passes the frame as an integer
+    (the reference declares c_double for OverlayAudioClip's i64, Pybind:577,
+    so the bool lands in the frame register) and AudioClip(rate, ch, data)
+    counts frames as len(data) // channels (the reference passes len(data),
+    Pybind:510, and reads past the buffer for ch > 1).
+Out of scope here (media back-end): VideoCap (FFmpeg).
 """
 from __future__ import annotations
 
@@ -46,15 +50,21 @@ def _f64_ptr(a: np.ndarray):
 class Helpers:
     @staticmethod
     def get_wappered_bytes_data_ptr(bytes: int):
-        raise NotImplementedError("WapperedBytes belong to the audio back-end (out of scope)")
+        return lib.GetWapperedBytesDataPtr(bytes)
 
     @staticmethod
     def get_wappered_bytes_data_size(bytes: int):
-        raise NotImplementedError("WapperedBytes belong to the audio back-end (out of scope)")
+        return lib.GetWapperedBytesDataSize(bytes)
 
     @staticmethod
     def wappered_bytes_to_python(bytes: int):
-        raise NotImplementedError("WapperedBytes belong to the audio back-end (out of scope)")
+        """Pybind:29-32; the WapperedBytes are released after the copy (the
+        reference leaks them)."""
+        ptr = Helpers.get_wappered_bytes_data_ptr(bytes)
+        size = Helpers.get_wappered_bytes_data_size(bytes)
+        out = ctypes.string_at(ptr, size)
+        lib.DestroyWapperedBytes(bytes)
+        return out
 
     @staticmethod
     def create_milthm_hit_effect_textures(mask: "Texture", n: int, seed: typing.Optional[float] = None):
@@ -553,6 +563,135 @@ class Comm:
         if getattr(self, "_ptr", None):
             lib.DestroyComm(self._ptr)
             self._ptr = None
+
+
+class AudioClip:
+    """Interleaved f64 samples in HBM (h:70-75); every operation is a kernel
+    on the device's stream (csrc/nr_audio.hip).  Mirrors Pybind:503-652."""
+
+    def __init__(self, sample_rate: int, channels: int, data: typing.Iterable[float]):
+        data = np.ascontiguousarray(np.asarray(data, dtype=np.float64).reshape(-1))
+        self._ptr = _check(lib.CreateAudioClipFromBuffer(sample_rate, channels, len(data) // max(channels, 1),
+                                                         _f64_ptr(data)), "CreateAudioClipFromBuffer")
+        self._update_props()
+
+    def _update_props(self):
+        self._sample_rate = lib.GetAudioClipSampleRate(self._ptr)
+        self._channels = lib.GetAudioClipChannels(self._ptr)
+        self._num_frames = lib.GetAudioClipNumFrames(self._ptr)
+
+    @staticmethod
+    def from_pydub_seg(seg):
+        from pydub import AudioSegment   # absent in this image, as in the reference's demo path
+
+        if not isinstance(seg, AudioSegment):
+            raise TypeError("seg must be a pydub.AudioSegment")
+        if seg.sample_width != 2:
+            seg = seg.set_sample_width(2)
+        data = seg.get_array_of_samples(array_type_override="h")
+        return Int16CreatedAudioClip(seg.frame_rate, seg.channels, data)
+
+    @staticmethod
+    def slient(sample_rate: int, channels: int, num_frames: int):   # sic: the reference's name (Pybind:544)
+        return PtrCreatedAudioClip(_check(lib.CreateSilentAudioClip(sample_rate, channels, num_frames),
+                                          "CreateSilentAudioClip"))
+
+    def clone(self):
+        return PtrCreatedAudioClip(_check(lib.CloneAudioClip(self._ptr), "CloneAudioClip"))
+
+    def resample(self, sample_rate: int, channels: int):
+        lib.ApplyResampleAudioClip(self._ptr, sample_rate, channels)
+        self._update_props()
+
+    def resample_like(clip: "AudioClip", like: "AudioClip"):
+        lib.ResampleAudioClipLike(clip._ptr, like._ptr)
+        clip._update_props()
+
+    @staticmethod
+    def _raise(res: int):
+        if res != 0:
+            if res == -1:
+                raise ValueError("target and source must have the same sample rate")
+            if res == -2:
+                raise ValueError("target and source must have the channels")
+            raise ValueError(f"unknown error code: {res} {_lib.last_error()}")
+
+    def overlay(target: "AudioClip", source: "AudioClip", start_time: typing.Union[int, float], *,
+                time_unit: typing.Literal["frame", "second"] = "frame", auto_resample: bool = False):
+        if time_unit not in ("frame", "second"):
+            raise ValueError("time_unit must be 'frame' or 'second'")
+        if time_unit == "frame":
+            res = lib.OverlayAudioClip(target._ptr, source._ptr, int(start_time), auto_resample)
+        else:
+            res = lib.OverlayAudioClipSecond(target._ptr, source._ptr, float(start_time), auto_resample)
+        AudioClip._raise(res)
+
+    def overlay_many(target: "AudioClip", source: "AudioClip", start_times: typing.Sequence[typing.Union[int, float]],
+                     *, time_unit: typing.Literal["frame", "second"] = "frame", auto_resample: bool = False):
+        """New: the same result as ``for t in start_times: target.overlay(source, t, ...)``, in one launch."""
+        if time_unit not in ("frame", "second"):
+            raise ValueError("time_unit must be 'frame' or 'second'")
+        if time_unit == "frame":
+            st = np.ascontiguousarray(np.asarray(start_times, dtype=np.int64).reshape(-1))
+            res = lib.OverlayAudioClipMany(target._ptr, source._ptr, st.ctypes.data_as(ctypes.c_void_p), len(st),
+                                           auto_resample)
+        else:
+            st = np.ascontiguousarray(np.asarray(start_times, dtype=np.float64).reshape(-1))
+            res = lib.OverlayAudioClipManySecond(target._ptr, source._ptr, _f64_ptr(st), len(st), auto_resample)
+        AudioClip._raise(res)
+
+    def save_as_wav(self):
+        return Helpers.wappered_bytes_to_python(lib.SaveAudioClipAsWav(self._ptr))
+
+    @property
+    def duration(self):
+        return lib.GetAudioClipDuration(self._ptr)
+
+    def apply_volume_gain(self, gain: float):
+        lib.ApplyVolumeGain(self._ptr, gain)
+
+    def cut(self, start: typing.Union[int, float], end: typing.Union[int, float], *,
+            time_unit: typing.Literal["frame", "second"] = "frame"):
+        if time_unit not in ("frame", "second"):
+            raise ValueError("time_unit must be 'frame' or 'second'")
+        if time_unit == "frame":
+            start, end = int(start), int(end)
+        else:
+            start, end = int(start * self._sample_rate), int(end * self._sample_rate)
+        lib.ApplyCutAudioClip(self._ptr, start, end)
+        self._update_props()
+
+    def apply_speed(self, speed: float):
+        lib.ApplySpeedAudioClip(self._ptr, speed)
+        self._update_props()
+
+    def to_numpy(self) -> np.ndarray:
+        """New: the samples as a (frames, channels) float64 array."""
+        self._update_props()
+        out = np.empty((self._num_frames, self._channels), dtype=np.float64)
+        if out.size:
+            lib.GetAudioClipBuffer(self._ptr, _f64_ptr(out))
+        return out
+
+    def __del__(self):
+        if getattr(self, "_ptr", None):
+            lib.DestroyAudioClip(self._ptr)
+            self._ptr = None
+
+
+class Int16CreatedAudioClip(AudioClip):
+    def __init__(self, sample_rate: int, channels: int, data: typing.Iterable[int]):
+        data = np.ascontiguousarray(np.asarray(data, dtype=np.int16).reshape(-1))
+        self._ptr = _check(lib.CreateAudioClipFromInt16Buffer(sample_rate, channels, len(data) // channels,
+                                                              data.ctypes.data_as(ctypes.c_void_p)),
+                           "CreateAudioClipFromInt16Buffer")
+        self._update_props()
+
+
+class PtrCreatedAudioClip(AudioClip):
+    def __init__(self, ptr: int):
+        self._ptr = ptr
+        self._update_props()
 
 
 def get_version():
