@@ -10,9 +10,9 @@
 // The mix is the hot part: thousands of OverlayAudioClip calls, each adding a
 // short clip into the song at a note time.  Sequential f64 adds do not
 // commute, so OverlayAudioClipMany (new) keeps the call order per sample: a
-// workgroup owns 256 consecutive samples of the target, finds the overlays
+// workgroup owns 1024 consecutive samples of the target, finds the overlays
 // touching them 256 starts at a time (ballot + prefix count into LDS, in call
-// order) and each thread adds its sample's contributions in that order —
+// order) and each thread adds its samples' contributions in that order —
 // identical to n calls of OverlayAudioClip, in one launch.
 //
 // Where the reference reads or writes outside a buffer (undefined behaviour)
@@ -121,19 +121,27 @@ __global__ void k_overlay(f64* __restrict__ tgt, i64 tgtFrames, const f64* __res
 }
 
 // n overlays of one source in call order (see the file comment).  Workgroup =
-// 256 consecutive target samples.
+// OV_PER x 256 consecutive target samples (thread: OV_PER samples 256 apart,
+// coalesced), so each scan of the start list serves 1024 samples.
+constexpr int OV_PER = 4;
 __global__ __launch_bounds__(AWG) void k_overlay_many(f64* __restrict__ tgt, i64 tgtFrames, const f64* __restrict__ src,
                                                       i64 srcFrames, i64 ch, const i64* __restrict__ starts, i64 n) {
     __shared__ i64 hit[AWG];
     __shared__ int wcnt[AWG / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const i64 total = tgtFrames * ch;
-    for (i64 e0 = (i64)blockIdx.x * AWG; e0 < total; e0 += (i64)gridDim.x * AWG) {
-        const i64 e = e0 + tid;
-        const bool live = e < total;
-        const i64 f = live ? e / ch : 0, c = live ? e - f * ch : 0;
-        const i64 fa = e0 / ch, fb = (min(e0 + AWG, total) - 1) / ch;   // frames this workgroup touches
-        f64 acc = live ? tgt[e] : 0.0;
+    constexpr i64 CH = (i64)AWG * OV_PER;
+    for (i64 e0 = (i64)blockIdx.x * CH; e0 < total; e0 += (i64)gridDim.x * CH) {
+        const i64 fa = e0 / ch, fb = ((e0 + CH < total ? e0 + CH : total) - 1) / ch;   // frames this chunk touches
+        f64 acc[OV_PER];
+        i64 fr[OV_PER], cc[OV_PER];
+#pragma unroll
+        for (int j = 0; j < OV_PER; ++j) {
+            const i64 e = e0 + j * AWG + tid;
+            fr[j] = e < total ? e / ch : -((i64)1 << 62);   // a dead slot matches no overlay
+            cc[j] = e < total ? e - fr[j] * ch : 0;
+            acc[j] = e < total ? tgt[e] : 0.0;
+        }
         for (i64 k0 = 0; k0 < n; k0 += AWG) {
             const i64 k = k0 + tid;
             bool h = false;
@@ -153,14 +161,21 @@ __global__ __launch_bounds__(AWG) void k_overlay_many(f64* __restrict__ tgt, i64
             }
             if (h) hit[base + __popcll(m & ((1ull << lane) - 1ull))] = s;
             __syncthreads();
-            if (live)
-                for (int q = 0; q < cnt; ++q) {
-                    const i64 i = f - hit[q];
-                    if (i >= 0 && i < srcFrames) acc += src[i * ch + c];
+            for (int q = 0; q < cnt; ++q) {
+                const i64 hs = hit[q];
+#pragma unroll
+                for (int j = 0; j < OV_PER; ++j) {
+                    const i64 i = fr[j] - hs;
+                    if (i >= 0 && i < srcFrames) acc[j] += src[i * ch + cc[j]];
                 }
+            }
             __syncthreads();
         }
-        if (live) tgt[e] = acc;
+#pragma unroll
+        for (int j = 0; j < OV_PER; ++j) {
+            const i64 e = e0 + j * AWG + tid;
+            if (e < total) tgt[e] = acc[j];
+        }
     }
 }
 
@@ -344,7 +359,7 @@ i64 OverlayAudioClipMany(AudioClip* target, AudioClip* source, const i64* startF
         i64* d = nullptr;
         NR_CHECK(hipMalloc((void**)&d, (size_t)n * sizeof(i64)));
         NR_CHECK(hipMemcpyAsync(d, startFrames, (size_t)n * sizeof(i64), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_overlay_many, dim3(grid_for(total)), dim3(AWG), 0, s, target->buffer, target->numFrames,
+        hipLaunchKernelGGL(k_overlay_many, dim3(grid_for((total + OV_PER - 1) / OV_PER)), dim3(AWG), 0, s, target->buffer, target->numFrames,
                            source->buffer, source->numFrames, source->channels, d, n);
         NR_CHECK(hipGetLastError());
         free_after(s, d);
