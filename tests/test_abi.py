@@ -35,6 +35,24 @@ REFERENCE_RENDER_SYMBOLS = [
 ]
 
 
+# The audio-clip entry points of the reference ABI (h:123-145) its AudioClip
+# class binds (Pybind.py:503-652); SURVEY §8f-4.
+REFERENCE_AUDIO_SYMBOLS = [
+    "GetAudioClipBufferSizeFromData", "GetAudioClipBufferSize", "CreateAudioClipFromBuffer",
+    "CreateAudioClipFromInt16Buffer", "CreateSilentAudioClip", "DestroyAudioClip", "CloneAudioClip",
+    "ApplyResampleAudioClip", "ResampleAudioClipLike", "OverlayAudioClip", "OverlayAudioClipSecond",
+    "SaveAudioClipAsWav", "GetAudioClipSampleRate", "GetAudioClipChannels", "GetAudioClipNumFrames",
+    "GetAudioClipDuration", "GetWapperedBytesDataPtr", "GetWapperedBytesDataSize", "ApplyVolumeGain",
+    "ApplyCutAudioClip", "ApplySpeedAudioClip",
+]
+
+
+def test_audio_symbols_declared_and_exported(hiplib):
+    assert set(REFERENCE_AUDIO_SYMBOLS) <= set(header_symbols())
+    for s in REFERENCE_AUDIO_SYMBOLS:
+        assert hasattr(hiplib, s), s
+
+
 @pytest.fixture(scope="module")
 def hiplib():
     from libnativecpurenderer_amd import _lib
