@@ -240,6 +240,134 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     }
 }
 
+// The same plan with one 256-thread workgroup (4 waves, <= 128 VGPRs, < 1 KB
+// LDS): it fits the slot a finishing k_vis workgroup frees, so it runs while
+// the previous batch's k_vis holds the chip (the 1024-thread plan needs a
+// whole CU and waits for k_vis to drain).  Each thread owns PS consecutive
+// tiles of a block of 256 * PS (thread-serial scan, then one workgroup scan).
+constexpr int PS_T = 256, PS_W = PS_T / 64, PS = 16;
+__global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
+                                                      u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
+                                                      u32* __restrict__ cur, u32* __restrict__ totals,
+                                                      u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
+                                                      u32 slice_target) {
+    __shared__ u32 sh[3][PS_W];
+    __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < PLAN_NB) bcnt[tid] = 0;
+    // pass 0: pair total (slice length) and dense-tile count
+    u32 a = 0, hv = 0;
+    for (int b0 = 0; b0 < ntiles; b0 += PS_T * PS) {
+        const int i0 = b0 + tid * PS;
+        u32 c[PS];
+#pragma unroll
+        for (int j = 0; j < PS; ++j) c[j] = i0 + j < ntiles ? cnt[i0 + j] : 0u;
+#pragma unroll
+        for (int j = 0; j < PS; ++j) {
+            a += c[j];
+            hv += c[j] >= HEAVY_PAIRS ? 1u : 0u;
+        }
+    }
+    a = wave_scan(a, lane); hv = wave_scan(hv, lane);
+    if (lane == 63) { sh[0][w] = a; sh[1][w] = hv; }
+    __syncthreads();
+    u32 ta = 0, th = 0;
+#pragma unroll
+    for (int k = 0; k < PS_W; ++k) { ta += sh[0][k]; th += sh[1][k]; }
+    u32 slice = SLICE_MIN;
+    while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
+    __syncthreads();
+    // pass 1: item totals and items per size class
+    u32 b = 0, m = 0;
+    for (int b0 = 0; b0 < ntiles; b0 += PS_T * PS) {
+        const int i0 = b0 + tid * PS;
+        u32 c[PS];
+#pragma unroll
+        for (int j = 0; j < PS; ++j) c[j] = i0 + j < ntiles ? cnt[i0 + j] : 0u;
+#pragma unroll
+        for (int j = 0; j < PS; ++j) {
+            if (i0 + j >= ntiles) break;
+            const u32 ni = tile_items(c[j], owned_row((i0 + j) / tiles_x, period, mask), slice);
+            b += ni;
+            m += c[j] > slice ? 1u : 0u;
+            if (ni) atomicAdd(&bcnt[size_class(c[j], slice)], ni);
+        }
+    }
+    b = wave_scan(b, lane); m = wave_scan(m, lane);
+    if (lane == 63) { sh[1][w] = b; sh[2][w] = m; }
+    __syncthreads();
+    u32 tb = 0, tm = 0;
+#pragma unroll
+    for (int k = 0; k < PS_W; ++k) { tb += sh[1][k]; tm += sh[2][k]; }
+    const bool fits = ta <= cap && tb <= icap;
+    if (tid == 0) {
+        u32 base = 0;
+        for (int k = PLAN_NB - 1; k >= 0; --k) { bcur[k] = base; base += bcnt[k]; }
+    }
+    __syncthreads();
+    // pass 2: offsets and items
+    u32 carry = 0;
+    for (int b0 = 0; b0 < ntiles; b0 += PS_T * PS) {
+        const int i0 = b0 + tid * PS;
+        u32 c[PS];
+#pragma unroll
+        for (int j = 0; j < PS; ++j) c[j] = i0 + j < ntiles ? cnt[i0 + j] : 0u;
+        u32 loc = 0;
+#pragma unroll
+        for (int j = 0; j < PS; ++j) loc += c[j];
+        const u32 inc = wave_scan(loc, lane);
+        if (lane == 63) sh[0][w] = inc;
+        __syncthreads();
+        u32 ea = carry + inc - loc;
+#pragma unroll
+        for (int k = 0; k < PS_W; ++k) {
+            if (k < w) ea += sh[0][k];
+            carry += sh[0][k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PS; ++j) {
+            const int i = i0 + j;
+            if (i >= ntiles) break;
+            off[i] = ea;
+            const u32 ni = tile_items(c[j], owned_row(i / tiles_x, period, mask), slice);
+            if (fits && ni) {
+                const u32 eb = atomicAdd(&bcur[size_class(c[j], slice)], ni);
+                for (u32 k = 0; k < ni; ++k) {
+                    const u32 ls = ea + k * slice;
+                    items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + c[j]), ni);
+                }
+            }
+            cnt[i] = 0;
+            cur[i] = 0;
+            ea += c[j];
+        }
+    }
+    if (tid == 0) {
+        off[ntiles] = ta;
+        const u32 t[4] = {ta, tb, tm, fits ? 1u : 0u};
+        for (int k = 0; k < 4; ++k) {
+            totals[k] = t[k];
+            __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Which plan kernel: the 256-thread one for unsharded frames (C3 0.167 ->
+// 0.160 ms per frame: it runs beside the previous k_vis), the 1024-thread one
+// for shards (a shard's k_vis is short, the plan mostly runs alone and the wider
+// workgroup is faster: 8-way share 0.0542 -> 0.0523 ms).  NR_PLAN_SMALL=0/1
+// forces one (A/B).
+static bool plan_small(int period) {
+    static const int v = [] {
+        const char* e = getenv("NR_PLAN_SMALL");
+        return e ? atoi(e) : -1;
+    }();
+    return v < 0 ? period == 1 : v != 0;
+}
+
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32* __restrict__ off,
                                                    u32* __restrict__ cur, u32* __restrict__ list, int ntiles,
@@ -957,9 +1085,14 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
-                           fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
-                           (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
+        if (plan_small(fp.period))
+            hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
+                               fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
+                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
+        else
+            hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
+                               fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
+                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_SCAN, e0, e1, sb);
 
