@@ -355,17 +355,18 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
     }
 }
 
-// Which plan kernel: the 256-thread one for unsharded frames (C3 0.167 ->
-// 0.160 ms per frame: it runs beside the previous k_vis), the 1024-thread one
-// for shards (a shard's k_vis is short, the plan mostly runs alone and the wider
-// workgroup is faster: 8-way share 0.0542 -> 0.0523 ms).  NR_PLAN_SMALL=0/1
-// forces one (A/B).
-static bool plan_small(int period) {
+// Which plan kernel: the 256-thread one for large unsharded batches (C3, 1M
+// triangles: 0.167 -> 0.160 ms per frame, the plan runs beside the previous
+// k_vis), the 1024-thread one otherwise: a shard's or a small batch's k_vis is
+// short, the plan mostly runs alone and the wider workgroup is faster (8-way C3
+// share 0.0542 -> 0.0523 ms; C2, 10k triangles, 0.0802 -> 0.0727 ms).
+// NR_PLAN_SMALL=0/1 forces one (A/B).
+static bool plan_small(int period, i64 ntri) {
     static const int v = [] {
         const char* e = getenv("NR_PLAN_SMALL");
         return e ? atoi(e) : -1;
     }();
-    return v < 0 ? period == 1 : v != 0;
+    return v < 0 ? period == 1 && ntri >= (1 << 18) : v != 0;
 }
 
 template <bool LDSH>
@@ -1085,7 +1086,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        if (plan_small(fp.period))
+        if (plan_small(fp.period, src.n))
             hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
                                (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
