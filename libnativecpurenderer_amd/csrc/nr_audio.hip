@@ -30,6 +30,8 @@
 #include "nr_common.h"
 
 #include <cstring>
+#include <atomic>
+#include <mutex>
 
 struct AudioClip {   // h:70-75, samples in HBM
     i64 sampleRate;
@@ -37,6 +39,9 @@ struct AudioClip {   // h:70-75, samples in HBM
     i64 numFrames;
     f64* buffer;     // device, numFrames * channels (at least one element allocated)
     int device;
+    u64 uid;         // never reused (keys the resample cache)
+    u64 version;     // bumped by every change of the samples or the rate
+    bool external;   // its device pointer was handed out: never cached
 };
 
 struct WapperedBytes {   // h:77-80, host bytes
@@ -199,10 +204,31 @@ __global__ void k_to_i16(const f64* __restrict__ p, short* __restrict__ out, i64
     }
 }
 
+std::mutex g_cache_mu;
+std::atomic<u64> g_clip_uid{0};
+
+// Resample cache for OverlayAudioClip(..., autoResample): the reference
+// clones and resamples the source on every call (cpp:1135-1143), so the demo's
+// 876 calls with one source (Pybind.py:693-695) resample it 876 times.  Here
+// the resampled copy is kept, keyed by (source uid, source version, target
+// rate and channels); any change of the source bumps its version, so a cached
+// copy always equals what a fresh clone + resample would give.
+struct CacheEntry {
+    u64 uid = 0, version = 0;
+    i64 rate = 0, channels = 0;
+    AudioClip* clip = nullptr;
+};
+constexpr int CACHE_N = 4;
+CacheEntry g_cache[CACHE_N];
+int g_cache_next = 0;
+
 AudioClip* new_clip(i64 rate, i64 ch, i64 frames) {
     AudioClip* a = new AudioClip();
     a->sampleRate = rate; a->channels = ch; a->numFrames = frames;
+    a->version = 0;
+    a->external = false;
     NR_CHECK(hipGetDevice(&a->device));
+    a->uid = ++g_clip_uid;
     a->buffer = alloc_samples(frames * ch, nr_stream_for(a->device));
     return a;
 }
@@ -216,6 +242,12 @@ void free_after(hipStream_t s, void* p) {
 hipStream_t clip_stream(AudioClip* a) {
     NR_CHECK(hipSetDevice(a->device));
     return nr_stream_for(a->device);
+}
+
+void destroy_clip(AudioClip* clip) {
+    hipStream_t s = clip_stream(clip);
+    free_after(s, clip->buffer);
+    delete clip;
 }
 
 }  // namespace
@@ -264,6 +296,14 @@ AudioClip* CreateSilentAudioClip(i64 sampleRate, i64 channels, i64 numFrames) {
 // cpp:1048-1052 is a no-op (the reference leaks); here the clip is freed
 void DestroyAudioClip(AudioClip* clip) {
     if (!clip) return;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);   // the resampled copies of this clip go with it
+        for (CacheEntry& e : g_cache)
+            if (e.clip && e.uid == clip->uid) {
+                destroy_clip(e.clip);
+                e = CacheEntry();
+            }
+    }
     hipStream_t s = clip_stream(clip);
     free_after(s, clip->buffer);
     delete clip;
@@ -299,6 +339,7 @@ void ApplyResampleAudioClip(AudioClip* clip, i64 sampleRate, i64 channels) {
     clip->sampleRate = sampleRate;
     clip->channels = channels;
     clip->numFrames = frames;
+    ++clip->version;
 }
 
 // cpp:1122-1127
@@ -307,8 +348,9 @@ void ResampleAudioClipLike(AudioClip* clip, AudioClip* like) {
 }
 
 // Shared front half of OverlayAudioClip(Many), cpp:1135-1143: the resampled
-// copy of `source` when asked for and needed (released by the caller; the
-// reference leaks it), or an error code.
+// copy of `source` when asked for and needed (from the resample cache; `tmp`
+// = an uncached copy the caller releases, for clips whose device pointer was
+// handed out; the reference leaks its copy), or an error code.
 static i64 overlay_source(AudioClip* target, AudioClip*& source, bool autoResample, AudioClip*& tmp) {
     tmp = nullptr;
     if (target->device != source->device) {
@@ -316,9 +358,25 @@ static i64 overlay_source(AudioClip* target, AudioClip*& source, bool autoResamp
         return -3;
     }
     if (autoResample && (target->sampleRate != source->sampleRate || target->channels != source->channels)) {
-        tmp = CloneAudioClip(source);
-        ResampleAudioClipLike(tmp, target);
-        source = tmp;
+        AudioClip* hit = nullptr;   // the caller holds g_cache_mu until its launch is queued
+        for (CacheEntry& e : g_cache)
+            if (e.clip && e.uid == source->uid && e.version == source->version && e.rate == target->sampleRate &&
+                e.channels == target->channels && e.clip->device == target->device)
+                hit = e.clip;
+        if (!hit) {
+            hit = CloneAudioClip(source);
+            ResampleAudioClipLike(hit, target);
+            if (source->external) {
+                tmp = hit;   // released by the caller
+            } else {
+                CacheEntry& e = g_cache[g_cache_next];
+                g_cache_next = (g_cache_next + 1) % CACHE_N;
+                AudioClip* old = e.clip;
+                e = {source->uid, source->version, target->sampleRate, target->channels, hit};
+                if (old) destroy_clip(old);
+            }
+        }
+        source = hit;
     }
     if (target->sampleRate != source->sampleRate) return -1;
     if (target->channels != source->channels) return -2;
@@ -328,6 +386,8 @@ static i64 overlay_source(AudioClip* target, AudioClip*& source, bool autoResamp
 // cpp:1129-1154
 i64 OverlayAudioClip(AudioClip* target, AudioClip* source, i64 startFrame, bool autoResample) {
     AudioClip* tmp;
+    std::unique_lock<std::mutex> lk(g_cache_mu, std::defer_lock);
+    if (autoResample) lk.lock();   // a cached copy is not evicted before the launch below is queued
     const i64 rc = overlay_source(target, source, autoResample, tmp);
     if (rc == 0) {
         hipStream_t s = clip_stream(target);
@@ -338,6 +398,8 @@ i64 OverlayAudioClip(AudioClip* target, AudioClip* source, i64 startFrame, bool 
             NR_CHECK(hipGetLastError());
         }
     }
+    if (rc == 0) ++target->version;
+    if (lk.owns_lock()) lk.unlock();
     if (tmp) DestroyAudioClip(tmp);
     return rc;
 }
@@ -352,6 +414,8 @@ i64 OverlayAudioClipSecond(AudioClip* target, AudioClip* source, f64 startSecond
 // return codes; the source is resampled at most once.
 i64 OverlayAudioClipMany(AudioClip* target, AudioClip* source, const i64* startFrames, i64 n, bool autoResample) {
     AudioClip* tmp;
+    std::unique_lock<std::mutex> lk(g_cache_mu, std::defer_lock);
+    if (autoResample) lk.lock();   // a cached copy is not evicted before the launch below is queued
     const i64 rc = overlay_source(target, source, autoResample, tmp);
     const i64 total = target->numFrames * target->channels;
     if (rc == 0 && n > 0 && total > 0 && source->numFrames > 0) {
@@ -365,6 +429,8 @@ i64 OverlayAudioClipMany(AudioClip* target, AudioClip* source, const i64* startF
         free_after(s, d);
         NR_CHECK(hipStreamSynchronize(s));   // caller owns startFrames
     }
+    if (rc == 0) ++target->version;
+    if (lk.owns_lock()) lk.unlock();
     if (tmp) DestroyAudioClip(tmp);
     return rc;
 }
@@ -433,6 +499,7 @@ void ApplyVolumeGain(AudioClip* clip, f64 gain) {
     hipStream_t s = clip_stream(clip);
     hipLaunchKernelGGL(k_gain, dim3(grid_for(n)), dim3(AWG), 0, s, clip->buffer, n, gain);
     NR_CHECK(hipGetLastError());
+    ++clip->version;
 }
 
 // cpp:1265-1279
@@ -450,11 +517,13 @@ void ApplyCutAudioClip(AudioClip* clip, i64 startFrame, i64 endFrame) {
     free_after(s, clip->buffer);
     clip->buffer = nb;
     clip->numFrames = frames;
+    ++clip->version;
 }
 
 // cpp:1281-1283: i64 *= f64 -> (i64)((f64)rate * speed)
 void ApplySpeedAudioClip(AudioClip* clip, f64 speed) {
     clip->sampleRate = nr_f2i64((f64)clip->sampleRate * speed);
+    ++clip->version;
 }
 
 // NEW: the clip's interleaved samples into a host buffer of
@@ -467,6 +536,15 @@ void GetAudioClipBuffer(AudioClip* clip, f64* out) {
 }
 
 // NEW: the device pointer of the samples (interop)
-void* GetAudioClipDevicePtr(AudioClip* clip) { return clip->buffer; }
+void* GetAudioClipDevicePtr(AudioClip* clip) {
+    clip->external = true;   // may change behind the library's back: its resampled copies are not cached
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    for (CacheEntry& e : g_cache)
+        if (e.clip && e.uid == clip->uid) {
+            destroy_clip(e.clip);
+            e = CacheEntry();
+        }
+    return clip->buffer;
+}
 
 }  // extern "C"

@@ -250,6 +250,8 @@ OPS = [
     ("overlay", 100, False),                       # rate mismatch: -1
     ("overlay", 100, True),                        # auto-resampled copy (48k mono -> 44.1k stereo)
     ("overlay_s", 0.25, True), ("overlay_s", 0.2500001, True),
+    ("hitgain", 0.5), ("overlay", 2000, True),       # the cached resampled copy must follow the source's change
+    ("speed", 1.0), ("overlay", 2500, True),
     ("like",), ("overlay", -700, False), ("overlay", 19000, False), ("overlay", 19000, False),
     ("overlay", 30000, False), ("clone_overlay", 5000),
     ("resample", 48000, 2), ("overlay", 10, False),   # -1 again: hit is at 44.1k
