@@ -29,6 +29,8 @@
 //                    it and resets those keys.
 #include "nr_tri.h"
 
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 #include <thread>
 
@@ -914,7 +916,8 @@ static u32 wide_heavy() {
 }
 
 template <int Z, bool C, bool G>
-void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid, hipStream_t s) {
+void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid, hipStream_t s,
+                hipEvent_t stop) {
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
     const bool coop = sc.coopMode ? sc.coopMode == 1
@@ -924,25 +927,37 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::F
     const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wide_heavy();
     if (wide) {
         if (coop)
-            hipLaunchKernelGGL((k_vis<Z, false, G, true, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, fp, F.fitems,
+            hipExtLaunchKernelGGL((k_vis<Z, false, G, true, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, nullptr, stop, 0, fp, F.fitems,
                                F.flist, sc.vis, sc.fdone, F.dplan);
         else
-            hipLaunchKernelGGL((k_vis<Z, false, G, false, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, fp, F.fitems,
+            hipExtLaunchKernelGGL((k_vis<Z, false, G, false, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, nullptr, stop, 0, fp, F.fitems,
                                F.flist, sc.vis, sc.fdone, F.dplan);
     } else if (coop) {
-        hipLaunchKernelGGL((k_vis<Z, C, G, true, VWG>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
+        hipExtLaunchKernelGGL((k_vis<Z, C, G, true, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.vis,
                            sc.fdone, F.dplan);
     } else {
-        hipLaunchKernelGGL((k_vis<Z, C, G, false, VWG>), dim3(grid), dim3(VWG), 0, s, fp, F.fitems, F.flist, sc.vis,
+        hipExtLaunchKernelGGL((k_vis<Z, C, G, false, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.vis,
                            sc.fdone, F.dplan);
     }
 }
 
 template <int Z, bool G>
 void launch_vis_z(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid,
-                  hipStream_t s) {
-    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, F, grid, s);
-    else launch_vis<Z, false, G>(fp, sc, F, grid, s);
+                  hipStream_t s, hipEvent_t stop) {
+    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, F, grid, s, stop);
+    else launch_vis<Z, false, G>(fp, sc, F, grid, s, stop);
+}
+
+// Events of a batch carried by the kernels' own completion signals
+// (hipExtLaunchKernel stop events) instead of separate marker packets: every
+// packet between two rasters on the main queue costs a few microseconds
+// (NR_EXT_STOP=0: hipEventRecord after the launch, for A/B).
+static bool ext_stop() {
+    static const bool v = [] {
+        const char* e = getenv("NR_EXT_STOP");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
 }
 
 // Everything a batch needs to be re-run after an overflow (nr_settle).
@@ -1117,24 +1132,30 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     }
 
     nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
-    if (ldsh) hipLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), hbytes, sb, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, F.dplan);
-    else hipLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, sb, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, F.dplan);
+    const bool xs = ext_stop() && sb != sa && !e1;   // no timing events around the kernel
+    hipEvent_t binStop = xs ? F.evBin : nullptr;
+    if (ldsh) hipExtLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), (u32)hbytes, sb, nullptr, binStop, 0, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, (const u32*)F.dplan);
+    else hipExtLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, sb, nullptr, binStop, 0, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, (const u32*)F.dplan);
     NR_CHECK(hipGetLastError());
     nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
     if (sb != sa) {
-        NR_CHECK(hipEventRecord(F.evBin, sb));
+        if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
         NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
     }
 
+    bool visDone = false;
     if (grid > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa); else launch_vis_z<1, false>(fp, sc, F, grid, sa); }
-        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa); else launch_vis_z<2, false>(fp, sc, F, grid, sa); }
-        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa); else launch_vis_z<0, false>(fp, sc, F, grid, sa); }
+        const bool vs = ext_stop() && !e1;
+        hipEvent_t st = vs ? F.evVis : nullptr;
+        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa, st); else launch_vis_z<1, false>(fp, sc, F, grid, sa, st); }
+        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa, st); else launch_vis_z<2, false>(fp, sc, F, grid, sa, st); }
+        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa, st); else launch_vis_z<0, false>(fp, sc, F, grid, sa, st); }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+        visDone = vs;
     }
-    NR_CHECK(hipEventRecord(F.evVis, sa));
+    if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
     F.visRecorded = true;
     return true;
 }
