@@ -118,7 +118,7 @@ DEVICE_ABI = {
 }
 
 # Audio clips (h:123-145).  OverlayAudioClip's startFrame is an
-# i64 here: the reference binding declares c_double for it (Pybind:577), which
+# i64 here: the reference binding declares c_double for it (Pybind:580), which
 # lands the bool in the i64 register (the frame-unit overlay is broken there).
 AUDIO_ABI = {
     "GetAudioClipBufferSizeFromData": (L, (L, L)),

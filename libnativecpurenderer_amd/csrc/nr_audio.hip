@@ -209,7 +209,7 @@ std::atomic<u64> g_clip_uid{0};
 
 // Resample cache for OverlayAudioClip(..., autoResample): the reference
 // clones and resamples the source on every call (cpp:1135-1143), so the demo's
-// 876 calls with one source (Pybind.py:693-695) resample it 876 times.  Here
+// 876 calls with one source (Pybind.py:689-691) resample it 876 times.  Here
 // the resampled copy is kept, keyed by (source uid, source version, target
 // rate and channels); any change of the source bumps its version, so a cached
 // copy always equals what a fresh clone + resample would give.

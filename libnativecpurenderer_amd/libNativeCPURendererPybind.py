@@ -17,7 +17,7 @@ Deliberate differences from the reference binding, each a reference bug:
     `c_double * len(data) // 8` precedence bug raises TypeError, :391);
   * apply_pixel works (the reference .so does not export ApplyPixel);
   * AudioClip.overlay(..., time_unit="frame") passes the frame as an integer
-    (the reference declares c_double for OverlayAudioClip's i64, Pybind:577,
+    (the reference declares c_double for OverlayAudioClip's i64, Pybind:580,
     so the bool lands in the frame register) and AudioClip(rate, ch, data)
     counts frames as len(data) // channels (the reference passes len(data),
     Pybind:510, and reads past the buffer for ch > 1).
@@ -567,7 +567,7 @@ class Comm:
 
 class AudioClip:
     """Interleaved f64 samples in HBM (h:70-75); every operation is a kernel
-    on the device's stream (csrc/nr_audio.hip).  Mirrors Pybind:503-652."""
+    on the device's stream (csrc/nr_audio.hip).  Mirrors Pybind:503-660."""
 
     def __init__(self, sample_rate: int, channels: int, data: typing.Iterable[float]):
         data = np.ascontiguousarray(np.asarray(data, dtype=np.float64).reshape(-1))

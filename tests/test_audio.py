@@ -10,7 +10,7 @@ and with the batched OverlayAudioClipMany.
 Parity unpinned by the reference: it has no audio test or fixture, its demo
 inputs are .ogg files that need FFmpeg/pydub (absent), and the reference C++
 cannot be built here.  test_files/audio_overlay_test.json (the
-reference demo's overlay times, Pybind.py:693-695) is read in this container
+reference demo's overlay times, Pybind.py:689-691) is read in this container
 as data: its 876 overlay times are committed as tests/golden/audio_overlay_times.json.
 """
 import ctypes
@@ -269,12 +269,12 @@ def test_audio_ops_match_oracle(both):
 
 # the reference demo's overlay times (876 seconds values): a copy of
 # /root/reference/test_files/audio_overlay_test.json, the data the demo at
-# Pybind.py:693-695 overlays audio2.ogg at
+# Pybind.py:689-691 overlays audio2.ogg at
 DEMO_TIMES = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "audio_overlay_times.json")))
 
 
 def mix(c: Clips, batched: bool):
-    """The reference demo's mix (Pybind.py:684-697: gains 0.7 / 1.1, one
+    """The reference demo's mix (Pybind.py:680-696: gains 0.7 / 1.1, one
     auto-resampled overlay per time of audio_overlay_test.json) on synthetic
     samples of the same shape (the .ogg inputs need FFmpeg), then milrenderer's
     note loop (milrenderer.py:803-815: drag sound resampled like the song,

@@ -1,4 +1,4 @@
-"""Audio mix benchmark: the reference demo's mix (Pybind.py:684-697:
+"""Audio mix benchmark: the reference demo's mix (Pybind.py:680-696:
 a song, gain 0.7, a hit sound with gain 1.1 overlaid with auto-resample at the
 876 times of test_files/audio_overlay_test.json) plus milrenderer's note loop
 (milrenderer.py:803-815), on synthetic samples of the same shape (114 s of
