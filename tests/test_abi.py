@@ -36,7 +36,7 @@ REFERENCE_RENDER_SYMBOLS = [
 
 
 # The audio-clip entry points of the reference ABI (h:123-145) its AudioClip
-# class binds (Pybind.py:503-652); SURVEY §8f-4.
+# class binds (Pybind.py:503-660); SURVEY §8f-4.
 REFERENCE_AUDIO_SYMBOLS = [
     "GetAudioClipBufferSizeFromData", "GetAudioClipBufferSize", "CreateAudioClipFromBuffer",
     "CreateAudioClipFromInt16Buffer", "CreateSilentAudioClip", "DestroyAudioClip", "CloneAudioClip",
