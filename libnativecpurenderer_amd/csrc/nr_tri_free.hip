@@ -357,18 +357,21 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
     }
 }
 
-// Which plan kernel: the 256-thread one for large unsharded batches (C3, 1M
-// triangles: 0.167 -> 0.160 ms per frame, the plan runs beside the previous
-// k_vis), the 1024-thread one otherwise: a shard's or a small batch's k_vis is
-// short, the plan mostly runs alone and the wider workgroup is faster (8-way C3
-// share 0.0542 -> 0.0523 ms; C2, 10k triangles, 0.0802 -> 0.0727 ms).
-// NR_PLAN_SMALL=0/1 forces one (A/B).
-static bool plan_small(int period, i64 ntri) {
+// Which plan kernel: the 256-thread one when the batch's owned share is large
+// (>= 2^17 triangles' worth: C3 unsharded 0.167 -> 0.160 ms per frame, C3 4-way
+// share 0.0654 -> 0.0627 ms; the plan runs beside the previous, long k_vis),
+// the 1024-thread one otherwise: a short k_vis leaves the plan mostly alone and
+// the wider workgroup is faster (C3 8-way share 0.0535 -> 0.0516 ms; C2, 10k
+// triangles, 0.0802 -> 0.069 ms).  NR_PLAN_SMALL=0/1 forces one (A/B).
+static bool plan_small(int period, u64 mask, i64 ntri) {
     static const int v = [] {
         const char* e = getenv("NR_PLAN_SMALL");
         return e ? atoi(e) : -1;
     }();
-    return v < 0 ? period == 1 && ntri >= (1 << 18) : v != 0;
+    if (v >= 0) return v != 0;
+    const u64 m = period >= 64 ? mask : (mask & ((1ull << period) - 1ull));
+    const f64 share = period == 1 ? 1.0 : (f64)__builtin_popcountll(m) / (f64)period;
+    return (f64)ntri * share >= (f64)(1 << 17);
 }
 
 template <bool LDSH>
@@ -1101,7 +1104,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        if (plan_small(fp.period, src.n))
+        if (plan_small(fp.period, fp.mask, src.n))
             hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
                                (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
