@@ -107,6 +107,19 @@ def test_c5_blend_overdraw_reduced(gpu, oracle):
     assert_same(g, o, "C5/10")
 
 
+@pytest.mark.slow
+def test_c5_blend_overdraw_full(gpu, oracle):
+    """C5 at its full size (BASELINE configs[4]: 50k large alpha-blended
+    triangles back to front, 1080p; ~1 G blended fragments, ~12 s on the
+    oracle), bit-exact f64 and depth."""
+    xy, z, c = scenes.triangle_soup(50000, 1920, 1080, 256, seed=1234, alpha=(0.2, 0.8))
+    order = np.argsort(-z.mean(axis=1), kind="stable")
+    xy, z, c = xy[order], z[order], c[order]
+    g, _ = _tri_frame(gpu, 1920, 1080, xy, z, c, write=False)
+    o, _ = _tri_frame(oracle, 1920, 1080, xy, z, c, write=False)
+    assert_same(g, o, "C5")
+
+
 def test_fragment_counter_matches_oracle(gpu, oracle):
     xy, z, c = scenes.triangle_soup(3000, 640, 480, 20, seed=8, gouraud=True)
     ctx = gpu.context(640, 480, False)
