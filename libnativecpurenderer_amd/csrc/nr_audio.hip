@@ -125,6 +125,20 @@ __global__ void k_overlay(f64* __restrict__ tgt, i64 tgtFrames, const f64* __res
     }
 }
 
+// A clip overlaid onto itself at start s > 0 (an echo): the reference's
+// loop reads samples it has already added to (cpp:1145-1151), so frame
+// s + i gets the updated frame i -- a recurrence along each chain r, r + s,
+// r + 2s, ... of stride s.  One thread per (chain, channel), sequential along
+// its chain; chains are independent.
+__global__ void k_overlay_self(f64* __restrict__ b, i64 frames, i64 ch, i64 s) {
+    const i64 n = s * ch;
+    for (i64 q = (i64)blockIdx.x * AWG + threadIdx.x; q < n; q += (i64)gridDim.x * AWG) {
+        const i64 r = q / ch, c = q - r * ch;
+        // source frame i = r + k*s updates target frame i + s, in increasing i
+        for (i64 i = r; i + s < frames; i += s) b[(i + s) * ch + c] += b[i * ch + c];
+    }
+}
+
 // n overlays of one source in call order (see the file comment).  Workgroup =
 // OV_PER x 256 consecutive target samples (thread: OV_PER samples 256 apart,
 // coalesced), so each scan of the start list serves 1024 samples.
@@ -389,8 +403,19 @@ i64 OverlayAudioClip(AudioClip* target, AudioClip* source, i64 startFrame, bool 
     std::unique_lock<std::mutex> lk(g_cache_mu, std::defer_lock);
     if (autoResample) lk.lock();   // a cached copy is not evicted before the launch below is queued
     const i64 rc = overlay_source(target, source, autoResample, tmp);
-    if (rc == 0) {
+    if (rc == 0 && source == target && startFrame > 0 && startFrame < target->numFrames) {
         hipStream_t s = clip_stream(target);
+        hipLaunchKernelGGL(k_overlay_self, dim3(grid_for(startFrame * target->channels)), dim3(AWG), 0, s,
+                           target->buffer, target->numFrames, target->channels, startFrame);
+        NR_CHECK(hipGetLastError());
+    } else if (rc == 0) {
+        hipStream_t s = clip_stream(target);
+        if (source == target && startFrame < 0 && !tmp) {
+            // reads run ahead of the writes in the reference's loop (every
+            // read sees the original sample): overlay from a copy
+            tmp = CloneAudioClip(target);
+            source = tmp;
+        }
         const i64 n = source->numFrames * source->channels;
         if (n > 0 && startFrame < target->numFrames) {
             hipLaunchKernelGGL(k_overlay, dim3(grid_for(n)), dim3(AWG), 0, s, target->buffer, target->numFrames,
@@ -418,6 +443,11 @@ i64 OverlayAudioClipMany(AudioClip* target, AudioClip* source, const i64* startF
     if (autoResample) lk.lock();   // a cached copy is not evicted before the launch below is queued
     const i64 rc = overlay_source(target, source, autoResample, tmp);
     const i64 total = target->numFrames * target->channels;
+    if (rc == 0 && source == target) {   // self-overlays depend on each other: one call at a time
+        if (lk.owns_lock()) lk.unlock();
+        for (i64 k = 0; k < n; ++k) OverlayAudioClip(target, target, startFrames[k], false);
+        return rc;
+    }
     if (rc == 0 && n > 0 && total > 0 && source->numFrames > 0) {
         hipStream_t s = clip_stream(target);
         i64* d = nullptr;

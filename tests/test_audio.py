@@ -370,3 +370,28 @@ def test_audioclip_python_surface(gpu):
     assert c._sample_rate == 16000 and c.duration == c._num_frames / 16000
     i16 = R.Int16CreatedAudioClip(8000, 2, np.arange(-50, 50, dtype=np.int16))
     assert np.array_equal(i16.to_numpy().reshape(-1), np.arange(-50, 50) / 32768.0)
+
+
+@pytest.mark.gpu
+def test_self_overlay_echo_matches_oracle(both):
+    """A clip overlaid onto itself: the reference's loop (cpp:1145-1151) reads
+    samples it has already added to when start > 0 (an echo recurrence) and
+    only original samples when start < 0."""
+    g, o = both
+    rng = np.random.default_rng(33)
+    data = rng.uniform(-0.5, 0.5, size=2 * 3001)
+    outs = []
+    for c in (g, o):
+        a = c.from_f64(22050, 2, data)
+        for st in (1, 37, 0, -20, 2999, 5000, -5000):
+            assert c.lib.OverlayAudioClip(a, a, st, True) == 0
+        starts = np.array([3, -2, 0, 1500], dtype=np.int64)
+        if c is g:
+            assert c.lib.OverlayAudioClipMany(a, a, _vp(starts), len(starts), False) == 0
+        else:
+            for s in starts:
+                assert c.lib.OverlayAudioClip(a, a, int(s), False) == 0
+        outs.append(c.samples(a))
+        c.lib.DestroyAudioClip(a)
+    bad = np.nonzero(bits(outs[0]) != bits(outs[1]))[0]
+    assert bad.size == 0, (bad.size, bad[:5])
