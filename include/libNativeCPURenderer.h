@@ -87,6 +87,7 @@ i64 OverlayAudioClipManySecond(AudioClip* target, AudioClip* source, const f64* 
 void DestroyWapperedBytes(WapperedBytes* bytes); /* NEW (the reference never frees them) */
 void GetAudioClipBuffer(AudioClip* clip, f64* out); /* NEW: samples to the host */
 void* GetAudioClipDevicePtr(AudioClip* clip);    /* NEW: samples in HBM (interop) */
+void SetAudioStreamOrderedAlloc(bool on);        /* NEW (tests): clip buffers from hipMallocAsync/hipFreeAsync */
 
 /* ---- texture preparation: procedural hit-effect shader (cpp:1318-1440) */
 Texture* CreateMilthmHitEffectTexture(Texture* mask, f64 seed, f64 t, f64 r, f64 g, f64 b); /* h:151; NULL
@@ -136,7 +137,8 @@ void GetDepthBuffer(RenderContext* ctx, uint32_t* out);                  /* NEW:
 void DrawTriangles(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba,
                    i64 n, bool gouraud);                                  /* NEW: host arrays */
 void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba,
-                         i64 n, bool gouraud);                            /* NEW: device pointers */
+                         i64 n, bool gouraud);                            /* NEW: device pointers; keep them valid
+                                 and unchanged until the batch has executed (Flush / readback / device sync) */
 TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f64* rgba,
                                      bool gouraud);                       /* NEW: one H2D upload */
 void DestroyTriangleBuffer(TriangleBuffer* tb);                          /* NEW */
@@ -163,7 +165,10 @@ void GetFrameU8(RenderContext* ctx, iu8* out);
 void* GetFrameU8DevicePtr(RenderContext* ctx);
 bool GetFrameYUV420P(RenderContext* ctx, iu8* out); /* §8f-2: YUV420P planes of that frame (W, H even), the
                                                        encoder input of PutRendererContextFrame (cpp:232-275) */
-bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root); /* f64 + depth bands to root */
+bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root); /* f64 + depth bands to root (a rank without
+                                                       a depth buffer sends its cleared one) */
+bool GatherFramebufferEx(RenderContext* ctx, NrComm* comm, i64 root, bool withDepth); /* withDepth: the same on
+                                                       every rank (it alone decides the posted send/recvs) */
 bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root); /* tests: GatherFrameU8's packed assembly of n
                                                                     shards of one process, device copies for RCCL */
 

@@ -104,6 +104,7 @@ DEVICE_ABI = {
     "GetFrameU8DevicePtr": (P, (P,)),
     "GetFrameYUV420P": (B, (P, P)),
     "GatherFramebuffer": (B, (P, P, L)),
+    "GatherFramebufferEx": (B, (P, P, L, B)),
     "GatherFrameU8Local": (B, (P, L, L)),
     "CreateMilthmHitEffectTextures": (B, (P, D, P, L, D, D, D, P)),
     "EnableKernelTiming": (None, (P, B)),
@@ -149,6 +150,7 @@ AUDIO_DEVICE_ABI = {
     "OverlayAudioClipMany": (L, (P, P, P, L, B)),
     "OverlayAudioClipManySecond": (L, (P, P, P, L, B)),
     "GetAudioClipDevicePtr": (P, (P,)),
+    "SetAudioStreamOrderedAlloc": (None, (B,)),
 }
 
 HIP_LIBRARY_ABI = {**REFERENCE_ABI, **TRIANGLE_ABI, **DEVICE_ABI, **AUDIO_ABI, **AUDIO_DEVICE_ABI}

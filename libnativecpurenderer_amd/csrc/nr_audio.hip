@@ -32,6 +32,7 @@
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <unordered_set>
 
 struct AudioClip {   // h:70-75, samples in HBM
     i64 sampleRate;
@@ -60,14 +61,35 @@ int grid_for(i64 n) {
     return (int)g;
 }
 
-// Plain hipMalloc/hipFree (hipFree waits for the device), not the stream-
-// ordered allocator: a mix run with hipMallocAsync/hipFreeAsync buffers once
-// read back a stale 32 MiB span of a clip (not reproduced since); the clip
-// operations are not latency-bound, so the simpler allocator is kept.
-f64* alloc_samples(i64 n, hipStream_t) {
-    f64* p = nullptr;
-    NR_CHECK(hipMalloc((void**)&p, (size_t)(n > 0 ? n : 1) * sizeof(f64)));
+// Sample and scratch buffers.  Every clip operation runs on the clip's
+// device stream (nr_stream_for) and every host-visible result is read back
+// after a synchronisation of that stream, so a buffer is only ever touched in
+// that one stream's order: no other library stream or the null stream reads
+// or writes it.  Default allocator: plain hipMalloc, freed after a stream
+// synchronisation.  Round 1 saw one mix run read back a stale 32 MiB span of a
+// clip with the stream-ordered allocator (hipMallocAsync / hipFreeAsync on the
+// same stream); SetAudioStreamOrderedAlloc(true) switches back to it so that
+// tests/test_audio.py::test_mix_with_stream_ordered_allocator can keep
+// checking the whole mix under it ("Audio clips").
+std::atomic<bool> g_async_alloc{false};
+std::mutex g_async_mu;
+std::unordered_set<void*> g_async_ptrs;   // buffers from hipMallocAsync
+
+void* alloc_bytes(size_t bytes, hipStream_t s) {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 8;
+    if (g_async_alloc.load()) {
+        NR_CHECK(hipMallocAsync(&p, bytes, s));
+        std::lock_guard<std::mutex> lk(g_async_mu);
+        g_async_ptrs.insert(p);
+    } else {
+        NR_CHECK(hipMalloc(&p, bytes));
+    }
     return p;
+}
+
+f64* alloc_samples(i64 n, hipStream_t s) {
+    return static_cast<f64*>(alloc_bytes((size_t)(n > 0 ? n : 1) * sizeof(f64), s));
 }
 
 // cpp:1029: (f64)v / 32768.0
@@ -122,6 +144,16 @@ __global__ void k_overlay(f64* __restrict__ tgt, i64 tgtFrames, const f64* __res
         const i64 t = start + i;
         if (t < 0 || t >= tgtFrames) continue;
         tgt[t * ch + c] += src[e];
+    }
+}
+
+// A clip overlaid onto itself at start 0: every sample is read once, then
+// written (cpp:1145-1151 with target == source), i.e. x + x.  Its own kernel:
+// k_overlay's __restrict__ operands must not alias.
+__global__ void k_overlay_same(f64* __restrict__ b, i64 n) {
+    for (i64 e = (i64)blockIdx.x * AWG + threadIdx.x; e < n; e += (i64)gridDim.x * AWG) {
+        const f64 v = b[e];
+        b[e] = v + v;
     }
 }
 
@@ -250,8 +282,18 @@ AudioClip* new_clip(i64 rate, i64 ch, i64 frames) {
     return a;
 }
 
-// frees a buffer the stream may still be using
+// frees a buffer the stream may still be using (stream-ordered when it came
+// from hipMallocAsync; otherwise after the stream drains)
 void free_after(hipStream_t s, void* p) {
+    {
+        std::lock_guard<std::mutex> lk(g_async_mu);
+        auto it = g_async_ptrs.find(p);
+        if (it != g_async_ptrs.end()) {
+            g_async_ptrs.erase(it);
+            NR_CHECK(hipFreeAsync(p, s));
+            return;
+        }
+    }
     NR_CHECK(hipStreamSynchronize(s));
     NR_CHECK(hipFree(p));
 }
@@ -291,8 +333,7 @@ AudioClip* CreateAudioClipFromInt16Buffer(i64 sampleRate, i64 channels, i64 numF
     hipStream_t s = nr_stream_for(a->device);
     const i64 n = numFrames * channels;
     if (n > 0) {
-        short* d = nullptr;
-        NR_CHECK(hipMalloc((void**)&d, (size_t)n * sizeof(short)));
+        short* d = static_cast<short*>(alloc_bytes((size_t)n * sizeof(short), s));
         NR_CHECK(hipMemcpyAsync(d, buffer, (size_t)n * sizeof(short), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_i16_to_f64, dim3(grid_for(n)), dim3(AWG), 0, s, d, a->buffer, n);
         NR_CHECK(hipGetLastError());
@@ -411,6 +452,12 @@ i64 OverlayAudioClip(AudioClip* target, AudioClip* source, i64 startFrame, bool 
         hipLaunchKernelGGL(k_overlay_self, dim3(grid_for(startFrame * target->channels)), dim3(AWG), 0, s,
                            target->buffer, target->numFrames, target->channels, startFrame);
         NR_CHECK(hipGetLastError());
+    } else if (rc == 0 && source == target && startFrame == 0) {
+        const i64 n = target->numFrames * target->channels;
+        if (n > 0) {
+            hipLaunchKernelGGL(k_overlay_same, dim3(grid_for(n)), dim3(AWG), 0, clip_stream(target), target->buffer, n);
+            NR_CHECK(hipGetLastError());
+        }
     } else if (rc == 0) {
         hipStream_t s = clip_stream(target);
         if (source == target && startFrame < 0 && !tmp) {
@@ -453,8 +500,7 @@ i64 OverlayAudioClipMany(AudioClip* target, AudioClip* source, const i64* startF
     }
     if (rc == 0 && n > 0 && total > 0 && source->numFrames > 0) {
         hipStream_t s = clip_stream(target);
-        i64* d = nullptr;
-        NR_CHECK(hipMalloc((void**)&d, (size_t)n * sizeof(i64)));
+        i64* d = static_cast<i64*>(alloc_bytes((size_t)n * sizeof(i64), s));
         NR_CHECK(hipMemcpyAsync(d, startFrames, (size_t)n * sizeof(i64), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_overlay_many, dim3(grid_for((total + OV_PER - 1) / OV_PER)), dim3(AWG), 0, s, target->buffer, target->numFrames,
                            source->buffer, source->numFrames, source->channels, d, n);
@@ -501,8 +547,7 @@ WapperedBytes* SaveAudioClipAsWav(AudioClip* clip) {
     put32(40, (int32_t)(n * 2));
     hipStream_t s = clip_stream(clip);
     if (n > 0) {
-        short* dv = nullptr;
-        NR_CHECK(hipMalloc((void**)&dv, (size_t)n * sizeof(short)));
+        short* dv = static_cast<short*>(alloc_bytes((size_t)n * sizeof(short), s));
         hipLaunchKernelGGL(k_to_i16, dim3(grid_for(n)), dim3(AWG), 0, s, clip->buffer, dv, n);
         NR_CHECK(hipGetLastError());
         NR_CHECK(hipMemcpyAsync(d + 44, dv, (size_t)n * sizeof(short), hipMemcpyDeviceToHost, s));
@@ -567,6 +612,10 @@ void GetAudioClipBuffer(AudioClip* clip, f64* out) {
     if (n > 0) NR_CHECK(hipMemcpyAsync(out, clip->buffer, (size_t)n * sizeof(f64), hipMemcpyDeviceToHost, s));
     NR_CHECK(hipStreamSynchronize(s));
 }
+
+// NEW (testing): sample and scratch buffers from the stream-ordered allocator
+// (hipMallocAsync / hipFreeAsync) instead of hipMalloc; see alloc_bytes.
+void SetAudioStreamOrderedAlloc(bool on) { g_async_alloc.store(on); }
 
 // NEW: the device pointer of the samples (interop)
 void* GetAudioClipDevicePtr(AudioClip* clip) {

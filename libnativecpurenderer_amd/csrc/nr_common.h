@@ -120,6 +120,7 @@ struct RenderContext {
     iu8* frameBuf[2] = {nullptr, nullptr};
     int frameCur = 0, frameLast = -1;            // buffer being rendered / of the last GatherFrameU8
     iu8* stageBuf[2] = {nullptr, nullptr}; size_t stageCap[2] = {0, 0};   // packed bands per buffer
+    iu8* yuvBuf = nullptr; size_t yuvCap = 0;    // GetFrameYUV420P planes (device)
     hipStream_t commStream = nullptr;            // RCCL transfers + the root's unpack
     hipEvent_t evFrameReady = nullptr, evGatherDone[2] = {nullptr, nullptr};
     bool gatherPending[2] = {false, false};

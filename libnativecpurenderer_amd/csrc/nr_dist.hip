@@ -537,15 +537,25 @@ bool GetFrameYUV420P(RenderContext* ctx, iu8* out) {
     if (ctx->frameLast < 0 || !ctx->frameBuf[ctx->frameLast] || W * H == 0) return W * H == 0;
     if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
     const size_t bytes = (size_t)(W * H + 2 * (W / 2) * (H / 2));
-    iu8* d = nullptr;
-    NR_CHECK(hipMallocAsync((void**)&d, bytes, ctx->stream));
+    if (bytes > ctx->yuvCap) {   // the context keeps its plane buffer (the stream has drained above)
+        NR_CHECK(hipStreamSynchronize(ctx->stream));
+        if (ctx->yuvBuf) NR_CHECK(hipFree(ctx->yuvBuf));
+        ctx->yuvBuf = nullptr;
+        ctx->yuvCap = 0;
+        if (hipMalloc((void**)&ctx->yuvBuf, bytes) != hipSuccess) {
+            nr_set_error_msg("GetFrameYUV420P: hipMalloc failed");
+            ctx->yuvBuf = nullptr;
+            return false;
+        }
+        ctx->yuvCap = bytes;
+    }
+    iu8* d = ctx->yuvBuf;
     const i64 blocks = (W / 2) * (H / 2);
     hipLaunchKernelGGL(k_yuv420p, dim3((unsigned)std::min<i64>((blocks + 255) / 256, 16384)), dim3(256), 0,
                        ctx->stream, ctx->frameBuf[ctx->frameLast], ctx->enableAlpha ? 4 : 3, W, H, d, d + W * H,
                        d + W * H + blocks);
     NR_CHECK(hipGetLastError());
     NR_CHECK(hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    NR_CHECK(hipFreeAsync(d, ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     return true;
 }
@@ -555,9 +565,13 @@ void* GetFrameU8DevicePtr(RenderContext* ctx) {
     return ctx->frameLast >= 0 ? ctx->frameBuf[ctx->frameLast] : ctx->frameU8;
 }
 
-// NEW: assemble the owned bands of the f64 framebuffer (and of the depth
-// buffer, when allocated) into the root's buffers — byte-exact N-GPU = 1-GPU.
-bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root) {
+// NEW: assemble the owned bands of the f64 framebuffer (and, with withDepth,
+// of the u32 depth buffer) into the root's buffers — byte-exact N-GPU =
+// 1-GPU.  Every rank must pass the same withDepth: the send/recv pairs of the
+// group are posted from it alone, never from a rank's own allocation state
+// (depth is allocated lazily, so ranks may differ there); a rank without a
+// depth buffer allocates its cleared one (all 0xFFFFFFFF) first.
+bool GatherFramebufferEx(RenderContext* ctx, NrComm* comm, i64 root, bool withDepth) {
     NR_CHECK(hipSetDevice(ctx->device));
     nr_materialize(ctx);
     if (!comm || comm->nranks == 1) return true;
@@ -565,8 +579,13 @@ bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root) {
         nr_set_error_msg("GatherFramebuffer: the context's shard must match the communicator");
         return false;
     }
+    if (root < 0 || root >= comm->nranks) {
+        nr_set_error_msg("GatherFramebuffer: root out of range");
+        return false;
+    }
     Rccl* r = rccl();
     if (!r) return false;
+    if (withDepth) nr_ensure_depth(ctx);
     const int ipp = ctx->enableAlpha ? 4 : 3;
     const i64 rowElems = ctx->width * ipp;
     const i64 bands = (ctx->height + BAND - 1) / BAND;
@@ -575,7 +594,7 @@ bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root) {
         const int owner = ctx->shardPattern[b % ctx->shardPeriod];
         const i64 rows = std::min<i64>(BAND, ctx->height - b * BAND);
         f64* p = ctx->buffer + b * BAND * rowElems;
-        u32* d = ctx->depth ? ctx->depth + b * BAND * ctx->width : nullptr;
+        u32* d = withDepth ? ctx->depth + b * BAND * ctx->width : nullptr;
         if (comm->rank == root && owner != root) {
             ok = nccl_ok(r, r->Recv(p, (size_t)(rows * rowElems), ncclFloat64, owner, comm->comm, ctx->stream), "ncclRecv");
             if (d && ok) ok = nccl_ok(r, r->Recv(d, (size_t)(rows * ctx->width), ncclUint32, owner, comm->comm, ctx->stream), "ncclRecv");
@@ -586,6 +605,11 @@ bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root) {
     }
     ok = nccl_ok(r, r->GroupEnd(), "ncclGroupEnd") && ok;
     return ok;
+}
+
+// NEW: GatherFramebufferEx with the depth bands always included.
+bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root) {
+    return GatherFramebufferEx(ctx, comm, root, true);
 }
 
 }  // extern "C"
@@ -606,6 +630,9 @@ void nr_dist_release(RenderContext* ctx) {
         ctx->evGatherDone[x] = nullptr;
     }
     ctx->frameU8 = nullptr;
+    if (ctx->yuvBuf) NR_CHECK(hipFree(ctx->yuvBuf));
+    ctx->yuvBuf = nullptr;
+    ctx->yuvCap = 0;
     if (ctx->evFrameReady) NR_CHECK(hipEventDestroy(ctx->evFrameReady));
     if (ctx->commStream) NR_CHECK(hipStreamDestroy(ctx->commStream));
     ctx->evFrameReady = nullptr;

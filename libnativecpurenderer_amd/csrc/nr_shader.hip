@@ -113,7 +113,7 @@ bool CreateMilthmHitEffectTextures(Texture* mask, f64 seed, const f64* ts, i64 n
         void* host = nullptr;
         void* dev = nullptr;
         NR_CHECK(hipHostMalloc(&host, bytes, hipHostMallocDefault));
-        NR_CHECK(hipMallocAsync(&dev, bytes, s));
+        NR_CHECK(hipMalloc(&dev, bytes));
         f64* hts = static_cast<f64*>(host);
         f64** hptr = reinterpret_cast<f64**>(hts + n);
         for (i64 k = 0; k < n; ++k) {
@@ -127,8 +127,8 @@ bool CreateMilthmHitEffectTextures(Texture* mask, f64 seed, const f64* ts, i64 n
         hipLaunchKernelGGL(k_hit_effect, dim3(grid), dim3(256), 0, s, mask->buffer, mask->width, mask->height, seed,
                            dts, dptr, (int)n, r, g, b);
         NR_CHECK(hipGetLastError());
-        NR_CHECK(hipFreeAsync(dev, s));
-        NR_CHECK(hipStreamSynchronize(s));   // the pinned staging is released below
+        NR_CHECK(hipStreamSynchronize(s));   // the device and pinned staging are released below
+        NR_CHECK(hipFree(dev));
         NR_CHECK(hipHostFree(host));
     }
     return true;
@@ -147,12 +147,12 @@ void GetMilthmHitEffectPixel(f64 seed, f64 t, f64 x, f64 y, f64* a) {
     NR_CHECK(hipGetDevice(&dev));
     hipStream_t s = nr_stream_for(dev);
     f64* d = nullptr;
-    NR_CHECK(hipMallocAsync(&d, sizeof(f64), s));
+    NR_CHECK(hipMalloc(&d, sizeof(f64)));
     hipLaunchKernelGGL(k_hit_pixel, dim3(1), dim3(1), 0, s, seed, t, x, y, d);
     NR_CHECK(hipGetLastError());
     NR_CHECK(hipMemcpyAsync(a, d, sizeof(f64), hipMemcpyDeviceToHost, s));
-    NR_CHECK(hipFreeAsync(d, s));
     NR_CHECK(hipStreamSynchronize(s));
+    NR_CHECK(hipFree(d));
 }
 
 }  // extern "C"

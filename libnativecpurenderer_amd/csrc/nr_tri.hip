@@ -115,7 +115,7 @@ Opacity device_opacity(RenderContext* ctx, const TriSrc& src) {
 }
 
 void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud, Opacity opq,
-          bool immutable = false) {
+          bool immutable = false, bool callerOwned = false) {
     NR_CHECK(hipSetDevice(ctx->device));
     settle(ctx);
     if (n <= 0 || ctx->width <= 0 || ctx->height <= 0) return;
@@ -123,7 +123,7 @@ void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 
     TriSrc src{xy, z, rgba, gouraud ? 1 : 0, n};
     const bool freeEligible = ctx->ct[3] == 1 && ctx->forceOrdered == 0;
     if (freeEligible && opq == OPQ_UNKNOWN) opq = device_opacity(ctx, src);
-    if (freeEligible && opq == OPQ_OPAQUE) draw_free(ctx, src, immutable);
+    if (freeEligible && opq == OPQ_OPAQUE) draw_free(ctx, src, immutable, callerOwned);
     else draw_ordered(ctx, src);
 }
 
@@ -163,7 +163,11 @@ void GetDepthBuffer(RenderContext* ctx, u32* out) {
 }
 
 // New: triangles from device-resident arrays (xy n*6, z n*3 or NULL,
-// rgba n*4 flat / n*12 Gouraud), in the context's transform.
+// rgba n*4 flat / n*12 Gouraud), in the context's transform.  Asynchronous
+// like any kernel launch: the arrays must stay valid and unchanged until the
+// batch has executed (Flush, a readback, or any device synchronisation).  The
+// visibility path sizes such a batch exactly inside this call (a host wait for
+// its binning), so nothing reads the arrays after that point.
 void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud) {
     // the kernels load positions and colours as 16-byte vectors: re-stage
     // arrays that are not 16-byte aligned (device-to-device copy)
@@ -179,10 +183,10 @@ void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const 
         f64* dc = dz + zn;
         NR_CHECK(hipMemcpyAsync(dxy, xy, (size_t)n * 6 * sizeof(f64), hipMemcpyDeviceToDevice, ctx->stream));
         NR_CHECK(hipMemcpyAsync(dc, rgba, (size_t)n * ncol * sizeof(f64), hipMemcpyDeviceToDevice, ctx->stream));
-        draw(ctx, dxy, z, dc, n, gouraud, OPQ_UNKNOWN);
+        draw(ctx, dxy, z, dc, n, gouraud, OPQ_UNKNOWN, false, z != nullptr);   // z stays the caller's
         return;
     }
-    draw(ctx, xy, z, rgba, n, gouraud, OPQ_UNKNOWN);
+    draw(ctx, xy, z, rgba, n, gouraud, OPQ_UNKNOWN, false, true);
 }
 
 // New: triangles from host arrays (copied to HBM first).

@@ -1165,7 +1165,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
 
 }  // namespace
 
-void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable) {
+void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable, bool callerOwned) {
     FrameParams fp = frame_params(ctx, src);
     if (ctx->frameOutput && fp.pendColor) {
         const size_t n = (size_t)(ctx->width * ctx->height * fp.ipp);
@@ -1176,8 +1176,11 @@ void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable) {
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
     bp.period = fp.period; bp.mask = fp.mask;
-    // fragment counting reads a counter back anyway: run exact (synchronous)
-    const bool exact = fp.fragCounter != nullptr;
+    // fragment counting reads a counter back anyway: run exact (synchronous);
+    // so does a batch from the caller's device arrays: a deferred overflow
+    // re-run (settle, at the next call) could read them after the caller has
+    // synchronised and released or rewritten them
+    const bool exact = fp.fragCounter != nullptr || callerOwned;
     TriScratch& sc = ctx->tri;
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % bin_sets();

@@ -274,8 +274,10 @@ class RenderContext:
         """DrawTrianglesDevice: the arrays already live in HBM on this
         context's device.  xy / rgba / z are device addresses (int) or objects
         with .data_ptr() (e.g. torch tensors, contiguous f64); layouts as
-        draw_triangles.  The call only enqueues work: keep the arrays alive
-        until the next sync point (flush / any readback)."""
+        draw_triangles.  The call enqueues work: keep the arrays alive and
+        unchanged until the batch has executed (flush, any readback, or a
+        device synchronisation such as torch.cuda.synchronize()); nothing
+        reads them after that (an overflowing batch is re-sized in the call)."""
         def addr(a):
             if a is None:
                 return None
@@ -373,9 +375,10 @@ class RenderContext:
             raise RuntimeError("GetFrameYUV420P failed: " + _lib.last_error())
         return out
 
-    def gather_framebuffer(self, comm: "Comm", root: int = 0):
-        """f64 framebuffer (+ depth) bands of every rank assembled on `root`."""
-        if not lib.GatherFramebuffer(self._ptr, comm._ptr, root):
+    def gather_framebuffer(self, comm: "Comm", root: int = 0, with_depth: bool = True):
+        """f64 framebuffer (+ depth) bands of every rank assembled on `root`
+        (with_depth must be the same on every rank)."""
+        if not lib.GatherFramebufferEx(self._ptr, comm._ptr, root, bool(with_depth)):
             raise RuntimeError("GatherFramebuffer failed: " + _lib.last_error())
 
     def last_raster_path(self) -> str:

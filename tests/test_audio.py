@@ -315,6 +315,28 @@ def test_hit_sound_mix_matches_oracle(both):
 
 
 @pytest.mark.gpu
+def test_mix_with_stream_ordered_allocator(both):
+    """round 1 saw one mix read back a stale 32 MiB span of a clip
+    while clip buffers came from hipMallocAsync/hipFreeAsync, and switched the
+    default to hipMalloc.  Every clip operation runs on the clip's one device
+    stream, so the stream-ordered allocator must give the same bits: run the
+    whole mix (call by call and batched, 80 MB song, many allocations and
+    stream-ordered frees) under it several times."""
+    g, o = both
+    og = mix(o, False)
+    g.lib.SetAudioStreamOrderedAlloc(True)
+    try:
+        for it in range(3):
+            for batched in (False, True):
+                gs, gw = mix(g, batched)
+                bad = np.nonzero(bits(gs) != bits(og[0]))[0]
+                assert bad.size == 0, (it, batched, bad.size, bad[:4], bad[-4:])
+                assert gw == og[1], (it, batched)
+    finally:
+        g.lib.SetAudioStreamOrderedAlloc(False)
+
+
+@pytest.mark.gpu
 def test_overlay_many_equals_calls_in_order(both):
     """Unsorted, repeated, negative and past-the-end starts; source longer than the target."""
     g, o = both

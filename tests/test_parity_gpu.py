@@ -395,6 +395,37 @@ def test_pair_list_overflow_is_rerun_in_order(gpu, oracle):
     assert_same(outs[0], outs[1], "overflow")
 
 
+def test_device_batch_overflow_never_rereads_caller_arrays(gpu, oracle):
+    """DrawTrianglesDevice on the caller's HBM tensors with an overflowing pair
+    list: the batch is sized exactly inside the call, so once the caller has
+    synchronised it may rewrite (or free) the tensors -- the next call on the
+    context must not re-run the batch from them."""
+    import torch
+    W, H = 260, 190
+    xy, z, c = scenes.triangle_soup(1500, W, H, 25, seed=62, gouraud=True)
+    want = {}
+    octx = oracle.context(W, H, False)
+    octx.set_color(0.2, 0.2, 0.2, 0.2)
+    octx.set_depth_state(True, True)
+    octx.clear_depth()
+    octx.draw_triangles(xy, c, z=z)
+    octx.draw_rect(30, 30, 80, 60, 0.9, 0.1, 0.1, 0.5)
+    want = {"f64": octx.get_buffer_numpy(), "depth": octx.get_depth_buffer()}
+    dxy, dz, dc = (torch.from_numpy(np.ascontiguousarray(a, np.float64).ravel()).to("cuda") for a in (xy, z, c))
+    torch.cuda.synchronize()
+    ctx = gpu.context(W, H, False)
+    ctx.set_pair_capacity_override(50)
+    ctx.set_color(0.2, 0.2, 0.2, 0.2)
+    ctx.set_depth_state(True, True)
+    ctx.clear_depth()
+    ctx.draw_triangles_device(dxy, dc, len(xy), z=dz, gouraud=True)
+    torch.cuda.synchronize()
+    dxy.fill_(float("nan")); dz.zero_(); dc.zero_()      # the caller reuses its tensors
+    torch.cuda.synchronize()
+    ctx.draw_rect(30, 30, 80, 60, 0.9, 0.1, 0.1, 0.5)
+    assert_same({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, want, "device overflow")
+
+
 def test_rotate_uses_sincos_like_the_reference_build(gpu, oracle):
     """cpp:436-444 compiled by g++ -O3 (src/compile.sh) calls glibc sincos(),
     which differs from separate sin/cos in the last bit for some angles: the
