@@ -61,14 +61,19 @@ def make_scene(cfg):
     return xy, z, c
 
 
-def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True):
+FRAME_OUT_BPP = {"rgb": 3.0, "yuv420p": 1.5}   # frame output bytes per pixel (RGB context)
+
+
+def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True, frame_out="rgb"):
     """B = N_tri*S_tri + W*H*(8*ipp + 4*[Z written]),
-    S_tri = 104 B flat / 168 B Gouraud; ipp = 3 (RGB); plus the 3 B/pixel u8
-    frame every step hands over (GetBufferAsUInt8 / GatherFrameU8).  `frac`:
-    the share of the frame one rank owns (tile-row shards)."""
+    S_tri = 104 B flat / 168 B Gouraud; ipp = 3 (RGB); plus the frame output
+    every step hands over: the 3 B/pixel u8 image (GetBufferAsUInt8 /
+    GatherFrameU8) or its 1.5 B/pixel YUV420P planes (--frame-output yuv420p).
+    `frac`: the share of the frame one rank owns (tile-row shards)."""
     s_tri = 168 if cfg["gouraud"] else 104
     zw = 4 if cfg.get("write", True) else 0
-    return int(frac * (n_tri * s_tri + cfg["W"] * cfg["H"] * (8 * 3 + zw + (3 if u8 else 0))))
+    out = FRAME_OUT_BPP[frame_out] if u8 else 0.0
+    return int(frac * (n_tri * s_tri + cfg["W"] * cfg["H"] * (8 * 3 + zw + out)))
 
 
 EVENT_EVERY = 10   # timed-region frames per HIP-event-timed frame of the dominant kernel (each record pair
@@ -77,13 +82,13 @@ EVENT_EVERY = 10   # timed-region frames per HIP-event-timed frame of the domina
 KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)"}
 
 
-def kernel_bytes(cfg, n_tri, path, frac=1.0):
+def kernel_bytes(cfg, n_tri, path, frac=1.0, frame_out="rgb"):
     """Algorithmic bytes of the dominant kernel per launch.
     Both rasterisers read each triangle (positions, depths, colours) once and
     write the framebuffer and depth once, all inside one kernel (k_vis shades
     its tiles itself; k_tile_raster keeps the tile in registers); k_vis also
     writes the u8 frame (k_to_u8_rows does it after the ordered raster)."""
-    return {"tile_raster": algorithmic_bytes(cfg, n_tri, frac, u8=(path == "order-free"))}
+    return {"tile_raster": algorithmic_bytes(cfg, n_tri, frac, u8=(path == "order-free"), frame_out=frame_out)}
 
 
 def cpu_baseline(cfg, xy, z, c, budget_s=10.0, max_frames=50):
@@ -130,6 +135,9 @@ def main():
     ap.add_argument("--gloo-test", action="store_true",
                     help="testing the N>1 orchestration on one GPU: gloo process group, CPU reductions, every rank "
                          "renders its shard on its LOCAL_RANK device but the RCCL frame gather is skipped")
+    ap.add_argument("--frame-output", default="rgb", choices=sorted(FRAME_OUT_BPP),
+                    help="frame output of every step: the u8 image (cpp:52-57) or its YUV420P planes (the video "
+                         "encoder's input, PutRendererContextFrame cpp:232-275), written by the raster and gathered")
     ap.add_argument("--root-slots", default="auto",
                     help="N>1 (and --emulate-shards): tile-row share of rank 0, in bands per 2 bands of every other "
                          "rank (SetShardSlots); 'equal' = SetShard; 'auto' (N>1) times candidates and keeps the "
@@ -160,6 +168,7 @@ def main():
     xy, z, c = make_scene(cfg)
     n_tri = len(xy)
     ctx = R.RenderContext(W, H, False)
+    ctx.set_frame_format(args.frame_output)
     if args.force_ordered:
         ctx.set_force_ordered_raster(True)
     buf = R.TriangleBuffer(xy, c, z=z, gouraud=cfg["gouraud"])
@@ -252,7 +261,7 @@ def main():
     path = ctx.last_raster_path()
     from libnativecpurenderer_amd import sharding
     frac = len(sharding.owned_rows(H, nsh, me, slots=slots_for(root_k) if nsh > 1 else None)) / H
-    kb = kernel_bytes(cfg, n_tri, path, frac)
+    kb = kernel_bytes(cfg, n_tri, path, frac, args.frame_output)
     dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
     # (2) timed region: K frames, HIP events only around the dominant kernel
@@ -278,7 +287,7 @@ def main():
     tot, cnt = ctx.get_kernel_timing(dom)
     dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
     achieved = kb[dom] / (dom_us * 1e-6) / 1e9
-    B = algorithmic_bytes(cfg, n_tri)   # whole job
+    B = algorithmic_bytes(cfg, n_tri, frame_out=args.frame_output)   # whole job
     traffic, pmc = load_pmc_traffic(args.config)
 
     if rank != 0:
@@ -299,6 +308,7 @@ def main():
         "data": "synthetic (deterministic displaced UV sphere / seeded soup, SURVEY.md §8d)",
         "config": {"workload": cfg["desc"], "width": W, "height": H, "triangles": n_tri,
                    "fragments_per_frame": int(frags), "frame_pixels": W * H,
+                   "frame_output": args.frame_output,
                    "parallelism": (f"tile-row shards x{world} + RCCL u8 frame gather" if world > 1
                                    else f"EMULATED shard 0 of {nsh} on one GPU (no gather)" if nsh > 1
                                    else "single GPU"),

@@ -163,6 +163,9 @@ i64 GetShardPattern(RenderContext* ctx, iu8* out64);   /* band b -> rank out64[b
 bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root);  /* u8 frame (cpp:52-57) assembled on root */
 void GetFrameU8(RenderContext* ctx, iu8* out);
 void* GetFrameU8DevicePtr(RenderContext* ctx);
+bool SetFrameFormat(RenderContext* ctx, i64 format); /* 0: u8 image (default), 1: YUV420P planes written by the
+                                                       raster and gathered as such (W, H even; same on all ranks) */
+i64 GetFrameFormat(RenderContext* ctx);
 bool GetFrameYUV420P(RenderContext* ctx, iu8* out); /* §8f-2: YUV420P planes of that frame (W, H even), the
                                                        encoder input of PutRendererContextFrame (cpp:232-275) */
 bool GatherFramebuffer(RenderContext* ctx, NrComm* comm, i64 root); /* f64 + depth bands to root (a rank without

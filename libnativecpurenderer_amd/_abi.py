@@ -103,6 +103,8 @@ DEVICE_ABI = {
     "GetFrameU8": (None, (P, P)),
     "GetFrameU8DevicePtr": (P, (P,)),
     "GetFrameYUV420P": (B, (P, P)),
+    "SetFrameFormat": (B, (P, L)),
+    "GetFrameFormat": (L, (P,)),
     "GatherFramebuffer": (B, (P, P, L)),
     "GatherFramebufferEx": (B, (P, P, L, B)),
     "GatherFrameU8Local": (B, (P, L, L)),

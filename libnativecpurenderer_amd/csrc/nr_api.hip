@@ -397,6 +397,7 @@ void ResizeRenderContext(RenderContext* ctx, i64 width, i64 height) {
     ctx->depth = nullptr;
     ctx->width = width;
     ctx->height = height;
+    if ((width & 1) || (height & 1)) ctx->frameFormat = 0;   // YUV420P needs even sizes (SetFrameFormat)
     ctx->pendColor = ctx->pendDepth = false;
     i64 n = GetBufferSize(ctx);
     NR_CHECK(hipMalloc(&ctx->buffer, (size_t)(n > 0 ? n : 1) * sizeof(f64)));

@@ -126,6 +126,10 @@ struct RenderContext {
     bool gatherPending[2] = {false, false};
     bool frameOutput = false;   // set by GatherFrameU8: resolves also write the u8 frame
     bool frameU8Valid = false;  // frameU8 holds the u8 image of every owned pixel
+    // frame output format (SetFrameFormat): 0 = the u8 image (cpp:52-57,
+    // W*H*ipp bytes), 1 = its YUV420P planes (Y W*H, U and V (W/2)*(H/2);
+    // W and H even), the encoder input of PutRendererContextFrame
+    int frameFormat = 0;
     void* pendingBatch = nullptr;   // last visibility batch awaiting validation (nr_settle)
     // deferred command list (BeginCommandList / EndCommandList, nr_prims.hip):
     // while recording, primitive draws are queued and run together, in
@@ -252,6 +256,30 @@ __host__ __device__ __forceinline__ u32 nr_quantize_depth(f64 z) {
 // truncation) unchanged.
 __device__ __forceinline__ u32 nr_quantize_depth_bl(f64 z) {
     return (u32)fmin(fmax(z * 4294967295.0, 0.0), 4294967295.0);
+}
+
+// Bytes of the context's frame output (frameFormat: u8 image or YUV420P).
+static inline i64 nr_frame_bytes(const RenderContext* ctx) {
+    const i64 W = ctx->width, H = ctx->height;
+    return ctx->frameFormat == 1 ? W * H + 2 * (W / 2) * (H / 2) : W * H * (ctx->enableAlpha ? 4 : 3);
+}
+
+// YUV420P of the u8 image (GetFrameYUV420P, SetFrameFormat): swscale's
+// unscaled RGB -> YV12 arithmetic (rgb2rgb rgb24toyv12): BT.601 limited
+// range, 15-bit coefficients (0.299/0.587/0.114 x 219/255, chroma x 224/255,
+// rounded), arithmetic shift, + 16 / 128; chroma point-sampled at the even
+// pixel of each 2x2 block.  Parity unpinned (FFmpeg absent).
+constexpr int NR_YRY = 8414, NR_YGY = 16519, NR_YBY = 3208;
+constexpr int NR_YRU = -4864, NR_YGU = -9527, NR_YBU = 14392;
+constexpr int NR_YRV = 14392, NR_YGV = -12060, NR_YBV = -2331;
+__host__ __device__ __forceinline__ iu8 nr_y_of(int r, int g, int b) {
+    return (iu8)(((NR_YRY * r + NR_YGY * g + NR_YBY * b) >> 15) + 16);
+}
+__host__ __device__ __forceinline__ iu8 nr_u_of(int r, int g, int b) {
+    return (iu8)(((NR_YRU * r + NR_YGU * g + NR_YBU * b) >> 15) + 128);
+}
+__host__ __device__ __forceinline__ iu8 nr_v_of(int r, int g, int b) {
+    return (iu8)(((NR_YRV * r + NR_YGV * g + NR_YBV * b) >> 15) + 128);
 }
 
 // cpp:52-57: (iu8)(v*255) = cvttsd2si to int32, keep the low byte (A.5)

@@ -109,10 +109,35 @@ __global__ void k_to_u8_rows(const f64* __restrict__ src, iu8* __restrict__ dst,
         dst[base + i] = nr_to_u8(src[base + i]);
 }
 
+// f64 -> YUV420P (SetFrameFormat(1)) over the owned tile rows: one thread per
+// 2x2 block, u8 per channel as cpp:52-57, then nr_y_of / nr_u_of / nr_v_of.
+__global__ void k_to_yuv_rows(const f64* __restrict__ src, iu8* __restrict__ dst, i64 W, i64 H, int ipp, int TH,
+                              int period, u64 mask) {
+    const i64 band = blockIdx.y;
+    if (period > 1 && !((mask >> (band % period)) & 1ull)) return;
+    const i64 r0 = band * TH;
+    if (r0 >= H) return;
+    const i64 rows = (H - r0) < TH ? (H - r0) : TH;
+    const i64 cw = W / 2, nb = (rows / 2) * cw;
+    iu8* up = dst + W * H;
+    iu8* vp = up + cw * (H / 2);
+    for (i64 q = (i64)blockIdx.x * blockDim.x + threadIdx.x; q < nb; q += (i64)gridDim.x * blockDim.x) {
+        const i64 cy = r0 / 2 + q / cw, cx = q % cw;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const i64 x = 2 * cx + (k & 1), y = 2 * cy + (k >> 1);
+            const f64* px = src + (y * W + x) * ipp;
+            const int r = nr_to_u8(px[0]), g = nr_to_u8(px[1]), b = nr_to_u8(px[2]);
+            dst[y * W + x] = nr_y_of(r, g, b);
+            if (k == 0) {
+                up[cy * cw + cx] = nr_u_of(r, g, b);
+                vp[cy * cw + cx] = nr_v_of(r, g, b);
+            }
+        }
+    }
+}
+
 // YUV420P from the u8 frame (GetFrameYUV420P): one thread per 2x2 block.
-constexpr int YRY = 8414, YGY = 16519, YBY = 3208;      // 0.299/0.587/0.114 * 219/255 * 2^15
-constexpr int YRU = -4864, YGU = -9527, YBU = 14392;    // -0.169/-0.331/0.5 * 224/255 * 2^15
-constexpr int YRV = 14392, YGV = -12060, YBV = -2331;   // 0.5/-0.419/-0.081 * 224/255 * 2^15
 __global__ void k_yuv420p(const iu8* __restrict__ rgb, int ipp, i64 W, i64 H, iu8* __restrict__ yp,
                           iu8* __restrict__ up, iu8* __restrict__ vp) {
     const i64 cw = W / 2, n = cw * (H / 2);
@@ -123,10 +148,10 @@ __global__ void k_yuv420p(const iu8* __restrict__ rgb, int ipp, i64 W, i64 H, iu
             const i64 x = 2 * cx + (k & 1), y = 2 * cy + (k >> 1);
             const iu8* px = rgb + (y * W + x) * ipp;
             const int r = px[0], g = px[1], b = px[2];
-            yp[y * W + x] = (iu8)(((YRY * r + YGY * g + YBY * b) >> 15) + 16);
+            yp[y * W + x] = nr_y_of(r, g, b);
             if (k == 0) {
-                up[q] = (iu8)(((YRU * r + YGU * g + YBU * b) >> 15) + 128);
-                vp[q] = (iu8)(((YRV * r + YGV * g + YBV * b) >> 15) + 128);
+                up[q] = nr_u_of(r, g, b);
+                vp[q] = nr_v_of(r, g, b);
             }
         }
     }
@@ -141,61 +166,109 @@ ShardMap shard_map(const RenderContext* ctx) {
     return m;
 }
 
-// Rows of the frame owned by `rank` under the context's band pattern.
-i64 owned_rows(const RenderContext* ctx, int rank) {
-    i64 rows = 0;
-    for (i64 b = 0; b * BAND < ctx->height; ++b)
-        if (ctx->shardPattern[b % ctx->shardPeriod] == rank) rows += std::min<i64>(BAND, ctx->height - b * BAND);
-    return rows;
+// Frame output geometry (nr_frame_bytes): the u8 image is one plane of
+// W*ipp bytes per row; YUV420P is Y (W per row) + U and V (W/2 per chroma
+// row, one chroma row per two rows).  Band b = rows [32b, 32b + 32) holds, in
+// the frame, up to three segments: its rows of each plane.
+struct FrameGeom {
+    i64 W, H;
+    int ipp;
+    int yuv;
+};
+
+FrameGeom frame_geom(const RenderContext* ctx) {
+    return FrameGeom{ctx->width, ctx->height, ctx->enableAlpha ? 4 : 3, ctx->frameFormat == 1 ? 1 : 0};
 }
 
-i64 max_owned_rows(const RenderContext* ctx, int n) {
+__host__ __device__ __forceinline__ int band_segments(const FrameGeom& g, i64 b, i64 (&off)[3], i64 (&len)[3]) {
+    const i64 r0 = b * BAND, rows = (g.H - r0) < BAND ? (g.H - r0) : BAND;
+    if (!g.yuv) {
+        off[0] = r0 * g.W * g.ipp;
+        len[0] = rows * g.W * g.ipp;
+        return 1;
+    }
+    const i64 cw = g.W / 2, c0 = r0 / 2, crows = rows / 2;
+    off[0] = r0 * g.W;                               len[0] = rows * g.W;
+    off[1] = g.W * g.H + c0 * cw;                    len[1] = crows * cw;
+    off[2] = g.W * g.H + (g.H / 2) * cw + c0 * cw;   len[2] = crows * cw;
+    return 3;
+}
+
+// Bytes of a full band (every band but possibly the frame's last).
+__host__ __device__ __forceinline__ i64 full_band_bytes(const FrameGeom& g) {
+    return g.yuv ? BAND * g.W + 2 * (BAND / 2) * (g.W / 2) : BAND * g.W * g.ipp;
+}
+
+// Bytes of the frame output owned by `rank` under the context's band pattern.
+i64 owned_bytes(const RenderContext* ctx, int rank) {
+    const FrameGeom g = frame_geom(ctx);
+    i64 bytes = 0;
+    for (i64 b = 0; b * BAND < ctx->height; ++b)
+        if (ctx->shardPattern[b % ctx->shardPeriod] == rank) {
+            i64 off[3], len[3];
+            const int ns = band_segments(g, b, off, len);
+            for (int k = 0; k < ns; ++k) bytes += len[k];
+        }
+    return bytes;
+}
+
+i64 max_owned_bytes(const RenderContext* ctx, int n) {
     i64 m = 0;
-    for (int p = 0; p < n; ++p) m = std::max(m, owned_rows(ctx, p));
+    for (int p = 0; p < n; ++p) m = std::max(m, owned_bytes(ctx, p));
     return m;
 }
 
 // Packed band layout of the gather: a rank's owned bands back to back (its
-// k-th band at k * BAND rows; only the frame's last band can be short, and it
-// is the last of its owner).  Pack (!UNPACK): the bands of `sel` from the
-// frame into `stage`.  Unpack: the bands of every rank but `root` from its
-// slot of `stage` (rank p at p * peerStride) into the frame.
+// k-th band at k * full_band_bytes, its segments one after another; only the
+// frame's last band can be short, and it is the last of its owner).  Pack
+// (!UNPACK): the bands of `sel` from the frame into `stage`.  Unpack: the
+// bands of every rank but `root` from its slot of `stage` (rank p at
+// p * peerStride) into the frame.
 template <typename V, bool UNPACK>
-__global__ void k_band_copy(iu8* __restrict__ frame, iu8* __restrict__ stage, i64 rowElems, i64 H, ShardMap sm,
-                            int sel, i64 peerStride) {
+__global__ void k_band_copy(iu8* __restrict__ frame, iu8* __restrict__ stage, FrameGeom g, ShardMap sm, int sel,
+                            i64 peerStride) {
     const i64 b = blockIdx.y;
     const int owner = sm.pattern[b % sm.period];
     if (UNPACK ? owner == sel : owner != sel) return;
-    const i64 r0 = b * BAND;
-    const i64 rows = (H - r0) < BAND ? (H - r0) : BAND;
-    const i64 n = rows * rowElems / (i64)sizeof(V);
-    V* f = reinterpret_cast<V*>(frame + r0 * rowElems);
-    V* s = reinterpret_cast<V*>(stage + (UNPACK ? owner * peerStride : 0) + band_index(sm, b, owner) * BAND * rowElems);
-    for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
-        if (UNPACK) f[i] = s[i];
-        else s[i] = f[i];
+    i64 off[3], len[3];
+    const int ns = band_segments(g, b, off, len);
+    iu8* sb = stage + (UNPACK ? owner * peerStride : 0) + band_index(sm, b, owner) * full_band_bytes(g);
+    for (int k = 0; k < ns; ++k) {
+        V* f = reinterpret_cast<V*>(frame + off[k]);
+        V* st = reinterpret_cast<V*>(sb);
+        const i64 n = len[k] / (i64)sizeof(V);
+        for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x) {
+            if (UNPACK) f[i] = st[i];
+            else st[i] = f[i];
+        }
+        sb += len[k];
     }
 }
 
-// Launches k_band_copy over every band on `st` (16-byte vectors when the row
-// length keeps every band 16-byte aligned).
-void band_copy(RenderContext* ctx, iu8* frame, iu8* stage, hipStream_t st, bool unpack, int sel, i64 peerStride,
-               i64 rowElems) {
+// Launches k_band_copy over every band on `st` (16-byte vectors when every
+// segment offset and length is a multiple of 16).
+void band_copy(RenderContext* ctx, iu8* frame, iu8* stage, hipStream_t st, bool unpack, int sel, i64 peerStride) {
     const ShardMap sm = shard_map(ctx);
+    const FrameGeom g = frame_geom(ctx);
     const i64 bands = (ctx->height + BAND - 1) / BAND;
-    const bool vec = rowElems % 16 == 0;
-    const i64 per = BAND * rowElems / (vec ? 16 : 1);
+    bool vec = full_band_bytes(g) % 16 == 0;
+    for (i64 b = 0; b < bands && vec; ++b) {
+        i64 off[3], len[3];
+        const int ns = band_segments(g, b, off, len);
+        for (int k = 0; k < ns; ++k) vec = vec && off[k] % 16 == 0 && len[k] % 16 == 0;
+    }
+    const i64 per = full_band_bytes(g) / (vec ? 16 : 1);
     dim3 grid((unsigned)std::min<i64>((per + 255) / 256, 1024), (unsigned)bands);
     if (vec) {
-        if (unpack) hipLaunchKernelGGL((k_band_copy<uint4, true>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                       ctx->height, sm, sel, peerStride);
-        else hipLaunchKernelGGL((k_band_copy<uint4, false>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                ctx->height, sm, sel, peerStride);
+        if (unpack) hipLaunchKernelGGL((k_band_copy<uint4, true>), grid, dim3(256), 0, st, frame, stage, g, sm, sel,
+                                       peerStride);
+        else hipLaunchKernelGGL((k_band_copy<uint4, false>), grid, dim3(256), 0, st, frame, stage, g, sm, sel,
+                                peerStride);
     } else {
-        if (unpack) hipLaunchKernelGGL((k_band_copy<iu8, true>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                       ctx->height, sm, sel, peerStride);
-        else hipLaunchKernelGGL((k_band_copy<iu8, false>), grid, dim3(256), 0, st, frame, stage, rowElems,
-                                ctx->height, sm, sel, peerStride);
+        if (unpack) hipLaunchKernelGGL((k_band_copy<iu8, true>), grid, dim3(256), 0, st, frame, stage, g, sm, sel,
+                                       peerStride);
+        else hipLaunchKernelGGL((k_band_copy<iu8, false>), grid, dim3(256), 0, st, frame, stage, g, sm, sel,
+                                peerStride);
     }
     NR_CHECK(hipGetLastError());
 }
@@ -247,7 +320,7 @@ void rotate_frame(RenderContext* ctx, int x) {
 bool frame_u8_local(RenderContext* ctx) {
     nr_materialize_color(ctx);
     const int ipp = ctx->enableAlpha ? 4 : 3;
-    const i64 n = ctx->width * ctx->height * ipp;
+    const i64 n = nr_frame_bytes(ctx);
     if (n <= 0) return true;
     if ((size_t)n > ctx->frameU8cap) {   // both frame buffers (the assembly alternates between them)
         if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
@@ -270,16 +343,23 @@ bool frame_u8_local(RenderContext* ctx) {
     }
     const i64 rowElems = ctx->width * ipp;
     const i64 bands = (ctx->height + BAND - 1) / BAND;
-    const i64 owned = owned_rows(ctx, ctx->shard);
-    // later triangle resolves write the u8 frame themselves (no re-read of
-    // the f64 frame); convert here only when that mirror is not current
+    const i64 owned = owned_bytes(ctx, ctx->shard);
+    // later triangle resolves write the frame output themselves (no re-read
+    // of the f64 frame); convert here only when that mirror is not current
     ctx->frameOutput = true;
     if (owned > 0 && !ctx->frameU8Valid) {
-        dim3 grid((unsigned)std::min<i64>((BAND * rowElems + 255) / 256, 4096), (unsigned)bands);
         hipEvent_t e0, e1;
         nr_timing_begin(ctx, NRK_OUTPUT, &e0, &e1);
-        hipLaunchKernelGGL(k_to_u8_rows, grid, dim3(256), 0, ctx->stream, ctx->buffer, ctx->frameU8, rowElems,
-                           ctx->height, BAND, ctx->shardPeriod, nr_shard_mask(ctx, ctx->shard));
+        if (ctx->frameFormat == 1) {
+            const i64 blocks = (BAND / 2) * (ctx->width / 2);
+            dim3 grid((unsigned)std::min<i64>((blocks + 255) / 256, 4096), (unsigned)bands);
+            hipLaunchKernelGGL(k_to_yuv_rows, grid, dim3(256), 0, ctx->stream, ctx->buffer, ctx->frameU8, ctx->width,
+                               ctx->height, ipp, BAND, ctx->shardPeriod, nr_shard_mask(ctx, ctx->shard));
+        } else {
+            dim3 grid((unsigned)std::min<i64>((BAND * rowElems + 255) / 256, 4096), (unsigned)bands);
+            hipLaunchKernelGGL(k_to_u8_rows, grid, dim3(256), 0, ctx->stream, ctx->buffer, ctx->frameU8, rowElems,
+                               ctx->height, BAND, ctx->shardPeriod, nr_shard_mask(ctx, ctx->shard));
+        }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_OUTPUT, e0, e1);
     }
@@ -417,22 +497,21 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
     // The transfer and the unpack run on the context's gather stream, so they
     // overlap the next frame, which renders into the other frame buffer.
     const int n = comm->nranks, me = comm->rank, x = ctx->frameCur;
-    const i64 rowElems = ctx->width * (ctx->enableAlpha ? 4 : 3);
-    const i64 peerStride = max_owned_rows(ctx, n) * rowElems;
+    const i64 peerStride = max_owned_bytes(ctx, n);
     ensure_comm_stream(ctx);
-    if (!ensure_stage(ctx, x, (size_t)(me == root ? n * peerStride : owned_rows(ctx, me) * rowElems)))
+    if (!ensure_stage(ctx, x, (size_t)(me == root ? n * peerStride : owned_bytes(ctx, me))))
         return false;
     iu8* frame = ctx->frameBuf[x];
     iu8* stage = ctx->stageBuf[x];
     hipEvent_t e0, e1;
     nr_timing_begin(ctx, NRK_GATHER, &e0, &e1);
-    if (me != root) band_copy(ctx, frame, stage, ctx->stream, false, me, 0, rowElems);
+    if (me != root) band_copy(ctx, frame, stage, ctx->stream, false, me, 0);
     nr_timing_end(ctx, NRK_GATHER, e0, e1);
     NR_CHECK(hipEventRecord(ctx->evFrameReady, ctx->stream));
     NR_CHECK(hipStreamWaitEvent(ctx->commStream, ctx->evFrameReady, 0));
     bool ok = nccl_ok(r, r->GroupStart(), "ncclGroupStart");
     for (int p = 0; p < n && ok; ++p) {
-        const size_t cnt = (size_t)(owned_rows(ctx, p) * rowElems);
+        const size_t cnt = (size_t)owned_bytes(ctx, p);
         if (cnt == 0) continue;
         if (me == root && p != root)
             ok = nccl_ok(r, r->Recv(stage + p * peerStride, cnt, ncclUint8, p, comm->comm, ctx->commStream),
@@ -441,7 +520,7 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
             ok = nccl_ok(r, r->Send(stage, cnt, ncclUint8, (int)root, comm->comm, ctx->commStream), "ncclSend");
     }
     ok = nccl_ok(r, r->GroupEnd(), "ncclGroupEnd") && ok;
-    if (ok && me == root) band_copy(ctx, frame, stage, ctx->commStream, true, (int)root, peerStride, rowElems);
+    if (ok && me == root) band_copy(ctx, frame, stage, ctx->commStream, true, (int)root, peerStride);
     rotate_frame(ctx, x);
     return ok;
 }
@@ -460,7 +539,8 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     for (i64 p = 0; p < n; ++p) {
         RenderContext* c = ctxs[p];
         if (c->nshards != n || c->shard != p || c->width != rc->width || c->height != rc->height ||
-            c->enableAlpha != rc->enableAlpha || c->device != rc->device || c->shardPeriod != rc->shardPeriod ||
+            c->enableAlpha != rc->enableAlpha || c->frameFormat != rc->frameFormat || c->device != rc->device ||
+            c->shardPeriod != rc->shardPeriod ||
             memcmp(c->shardPattern, rc->shardPattern, 64) != 0) {
             nr_set_error_msg("GatherFrameU8Local: ctxs[p] must be shard p of n (one pattern), all of one size and device");
             return false;
@@ -469,8 +549,7 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
         if (!frame_u8_local(c)) return false;
     }
     if (n == 1) return true;
-    const i64 rowElems = rc->width * (rc->enableAlpha ? 4 : 3);
-    const i64 peerStride = max_owned_rows(rc, (int)n) * rowElems;
+    const i64 peerStride = max_owned_bytes(rc, (int)n);
     NR_CHECK(hipSetDevice(rc->device));
     ensure_comm_stream(rc);
     const int xr = rc->frameCur;
@@ -480,9 +559,9 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
         RenderContext* c = ctxs[p];
         ensure_comm_stream(c);
         const int xp = c->frameCur;
-        const size_t cnt = (size_t)(owned_rows(c, (int)p) * rowElems);
+        const size_t cnt = (size_t)owned_bytes(c, (int)p);
         if (!ensure_stage(c, xp, cnt)) return false;
-        band_copy(c, c->frameBuf[xp], c->stageBuf[xp], c->stream, false, (int)p, 0, rowElems);
+        band_copy(c, c->frameBuf[xp], c->stageBuf[xp], c->stream, false, (int)p, 0);
         NR_CHECK(hipEventRecord(c->evFrameReady, c->stream));
         NR_CHECK(hipStreamWaitEvent(rc->commStream, c->evFrameReady, 0));
         NR_CHECK(hipMemcpyAsync(rc->stageBuf[xr] + p * peerStride, c->stageBuf[xp], cnt, hipMemcpyDeviceToDevice,
@@ -490,7 +569,7 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     }
     NR_CHECK(hipEventRecord(rc->evFrameReady, rc->stream));
     NR_CHECK(hipStreamWaitEvent(rc->commStream, rc->evFrameReady, 0));
-    band_copy(rc, rc->frameBuf[xr], rc->stageBuf[xr], rc->commStream, true, (int)root, peerStride, rowElems);
+    band_copy(rc, rc->frameBuf[xr], rc->stageBuf[xr], rc->commStream, true, (int)root, peerStride);
     // the peers' stages were read on the root's gather stream: their own
     // gather streams (whose events guard the buffers' reuse) wait for it
     NR_CHECK(hipEventRecord(rc->evGatherDone[xr], rc->commStream));
@@ -510,8 +589,7 @@ void GetFrameU8(RenderContext* ctx, iu8* out) {
     NR_CHECK(hipSetDevice(ctx->device));
     if (ctx->frameLast < 0 || !ctx->frameBuf[ctx->frameLast]) return;
     if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
-    NR_CHECK(hipMemcpyAsync(out, ctx->frameBuf[ctx->frameLast],
-                            (size_t)(ctx->width * ctx->height * (ctx->enableAlpha ? 4 : 3)), hipMemcpyDeviceToHost,
+    NR_CHECK(hipMemcpyAsync(out, ctx->frameBuf[ctx->frameLast], (size_t)nr_frame_bytes(ctx), hipMemcpyDeviceToHost,
                             ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));
 }
@@ -537,6 +615,11 @@ bool GetFrameYUV420P(RenderContext* ctx, iu8* out) {
     if (ctx->frameLast < 0 || !ctx->frameBuf[ctx->frameLast] || W * H == 0) return W * H == 0;
     if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
     const size_t bytes = (size_t)(W * H + 2 * (W / 2) * (H / 2));
+    if (ctx->frameFormat == 1) {   // the frame output already is YUV420P
+        NR_CHECK(hipMemcpyAsync(out, ctx->frameBuf[ctx->frameLast], bytes, hipMemcpyDeviceToHost, ctx->stream));
+        NR_CHECK(hipStreamSynchronize(ctx->stream));
+        return true;
+    }
     if (bytes > ctx->yuvCap) {   // the context keeps its plane buffer (the stream has drained above)
         NR_CHECK(hipStreamSynchronize(ctx->stream));
         if (ctx->yuvBuf) NR_CHECK(hipFree(ctx->yuvBuf));
@@ -559,6 +642,35 @@ bool GetFrameYUV420P(RenderContext* ctx, iu8* out) {
     NR_CHECK(hipStreamSynchronize(ctx->stream));
     return true;
 }
+
+// NEW: format of the frame output of GatherFrameU8 / GatherFrameU8Local:
+// 0 = the u8 image (cpp:52-57, default), 1 = its YUV420P planes (the encoder
+// input of PutRendererContextFrame, cpp:232-275; 1.5 bytes per pixel instead
+// of 3 or 4 through the gather and to the host).  The raster writes it
+// directly.  Every rank of a frame must use the same format;
+// YUV420P needs even W and H.
+bool SetFrameFormat(RenderContext* ctx, i64 format) {
+    if (format != 0 && format != 1) {
+        nr_set_error_msg("SetFrameFormat: 0 (u8 image) or 1 (YUV420P)");
+        return false;
+    }
+    if (format == 1 && ((ctx->width & 1) || (ctx->height & 1))) {
+        nr_set_error_msg("SetFrameFormat: YUV420P needs even width and height");
+        return false;
+    }
+    if (ctx->frameFormat != (int)format) {
+        NR_CHECK(hipSetDevice(ctx->device));
+        nr_settle(ctx);
+        nr_dist_sync(ctx);
+        ctx->frameFormat = (int)format;
+        ctx->frameU8Valid = false;
+        ctx->frameLast = -1;
+        for (bool& g : ctx->gatherPending) g = false;
+    }
+    return true;
+}
+
+i64 GetFrameFormat(RenderContext* ctx) { return ctx->frameFormat; }
 
 // NEW: device pointer of that frame (complete once Flush returns).
 void* GetFrameU8DevicePtr(RenderContext* ctx) {

@@ -233,7 +233,9 @@ struct FrameParams {
     int pendDepth;
     u32 pendDepthValue;
     unsigned long long* fragCounter;   // non-null: count covered fragments
-    iu8* frameU8;                      // non-null: resolve also writes the u8 frame (cpp:52-57)
+    iu8* frameU8;                      // non-null: resolve also writes the frame output: the u8
+                                       // image (cpp:52-57), or with frameYUV its YUV420P planes
+    int frameYUV;
 };
 
 enum Opacity { OPQ_UNKNOWN = 0, OPQ_OPAQUE, OPQ_BLENDED };

@@ -50,6 +50,7 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src) {
     fp.pendDepthValue = ctx->pendDepthValue;
     fp.fragCounter = nullptr;
     fp.frameU8 = nullptr;
+    fp.frameYUV = ctx->frameFormat == 1;
     if (ctx->countFragments) {
         if (!sc.d_frag) NR_CHECK(hipMalloc(&sc.d_frag, sizeof(u64)));
         NR_CHECK(hipMemsetAsync(sc.d_frag, 0, sizeof(u64), ctx->stream));

@@ -469,16 +469,31 @@ __device__ __forceinline__ void store_depth(const FrameParams& fp, i64 p, u64 kv
     else if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
 }
 
-// Framebuffer (+ u8 frame) value of a pixel, written once.
-__device__ __forceinline__ void store_colour(const FrameParams& fp, i64 p, f64 cr, f64 cg, f64 cb, f64 ca) {
+// Framebuffer (+ frame output) value of pixel p = (px, py), written once.
+// The frame output is the u8 image (cpp:52-57) or, with fp.frameYUV, its
+// YUV420P planes: Y of every pixel, U and V from the even pixel of each 2x2
+// block (tiles have even sizes and origins, so a block never straddles two).
+__device__ __forceinline__ void store_colour(const FrameParams& fp, i64 p, i64 px, i64 py, f64 cr, f64 cg, f64 cb,
+                                             f64 ca) {
     const int ipp = fp.ipp;
     f64* dst = fp.fb + p * ipp;
     dst[0] = cr; dst[1] = cg; dst[2] = cb;
     if (ipp == 4) dst[3] = ca;
     if (fp.frameU8) {
-        iu8* d8 = fp.frameU8 + p * ipp;
-        d8[0] = nr_to_u8(cr); d8[1] = nr_to_u8(cg); d8[2] = nr_to_u8(cb);
-        if (ipp == 4) d8[3] = nr_to_u8(ca);
+        const int r8 = nr_to_u8(cr), g8 = nr_to_u8(cg), b8 = nr_to_u8(cb);
+        if (fp.frameYUV) {
+            fp.frameU8[p] = nr_y_of(r8, g8, b8);
+            if (!((px | py) & 1)) {
+                const i64 cw = fp.W >> 1;
+                iu8* up = fp.frameU8 + fp.W * fp.H + (py >> 1) * cw + (px >> 1);
+                up[0] = nr_u_of(r8, g8, b8);
+                up[cw * (fp.H >> 1)] = nr_v_of(r8, g8, b8);
+            }
+        } else {
+            iu8* d8 = fp.frameU8 + p * ipp;
+            d8[0] = (iu8)r8; d8[1] = (iu8)g8; d8[2] = (iu8)b8;
+            if (ipp == 4) d8[3] = nr_to_u8(ca);
+        }
     }
 }
 
@@ -502,10 +517,10 @@ __device__ __forceinline__ void apply_winner(const FrameParams& fp, i64 p, f64& 
 
 // Pending clears of a pixel no fragment won.
 template <int ZMODE>
-__device__ __forceinline__ void store_clear(const FrameParams& fp, i64 p) {
+__device__ __forceinline__ void store_clear(const FrameParams& fp, i64 p, i64 px, i64 py) {
     if (fp.pendColor) {
         const f64 v = fp.pendColorValue;
-        store_colour(fp, p, v, v, v, v);
+        store_colour(fp, p, px, py, v, v, v, v);
     }
     store_depth<ZMODE>(fp, p, 0);
 }
@@ -617,7 +632,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         if (!id) {
             if (fp.pendColor) {
                 const f64 v = fp.pendColorValue;
-                store_colour(fp, gp, v, v, v, v);
+                store_colour(fp, gp, px, py, v, v, v, v);
             }
             continue;
         }
@@ -637,7 +652,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
             record_colour<GOURAUD>(r, px, py, cr, cg, cb, ca);
         }
         apply_winner(fp, gp, cr, cg, cb, ca);
-        store_colour(fp, gp, cr, cg, cb, ca);
+        store_colour(fp, gp, px, py, cr, cg, cb, ca);
     }
 }
 
@@ -724,7 +739,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
         if (ls == le) {   // no triangle: only the pending clears
             for (int p = tid; p < TH * TW; p += NT) {
                 const int lx = p & (TW - 1), ly = p / TW;
-                if (lx < wlim && ly < hlim) store_clear<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx);
+                if (lx < wlim && ly < hlim)
+                    store_clear<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx, x0 + lx, y0 + ly);
             }
             continue;
         }
@@ -1168,7 +1184,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
 void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable, bool callerOwned) {
     FrameParams fp = frame_params(ctx, src);
     if (ctx->frameOutput && fp.pendColor) {
-        const size_t n = (size_t)(ctx->width * ctx->height * fp.ipp);
+        const size_t n = (size_t)nr_frame_bytes(ctx);
         if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
     }
     BinParams bp;

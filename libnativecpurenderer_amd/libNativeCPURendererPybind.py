@@ -352,10 +352,22 @@ class RenderContext:
             raise RuntimeError("GatherFrameU8 failed: " + _lib.last_error())
 
     def get_frame_u8(self) -> np.ndarray:
-        ipp = 4 if self.enable_alpha else 3
-        out = np.empty((self.height, self.width, ipp), dtype=np.uint8)
+        """The frame output of the last gather: the (H, W, ipp) u8 image, or
+        with set_frame_format("yuv420p") the flat Y, U, V planes."""
+        if lib.GetFrameFormat(self._ptr) == 1:
+            out = np.empty(self.width * self.height + 2 * (self.width // 2) * (self.height // 2), dtype=np.uint8)
+        else:
+            out = np.empty((self.height, self.width, 4 if self.enable_alpha else 3), dtype=np.uint8)
         lib.GetFrameU8(self._ptr, out.ctypes.data_as(ctypes.c_void_p))
         return out
+
+    def set_frame_format(self, fmt: str):
+        """Frame output of gather_frame_u8: "rgb" (the u8 image, cpp:52-57;
+        default) or "yuv420p" (its YUV420P planes, the video encoder's input,
+        written directly by the raster; even W and H)."""
+        code = {"rgb": 0, "yuv420p": 1}[fmt]
+        if not lib.SetFrameFormat(self._ptr, code):
+            raise RuntimeError("SetFrameFormat failed: " + _lib.last_error())
 
     @staticmethod
     def gather_frame_u8_local(ctxs: typing.Sequence["RenderContext"], root: int = 0):

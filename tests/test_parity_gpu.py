@@ -296,17 +296,23 @@ def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque):
                                                            (8, 0, 256, 300, False, None), (8, 5, 100, 40, False, None),
                                                            (2, 0, 256, 500, False, [5, 1]),
                                                            (4, 2, 333, 700, True, [1, 2, 6, 3]),
-                                                           (8, 0, 512, 1000, False, [6, 2, 2, 2, 2, 2, 2, 2])])
-def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha, slots):
+                                                           (8, 0, 512, 1000, False, [6, 2, 2, 2, 2, 2, 2, 2]),
+                                                           (3, 1, 334, 250, False, None)])
+@pytest.mark.parametrize("fmt", ["rgb", "yuv420p"])
+def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha, slots, fmt):
     """GatherFrameU8's assembly (each rank's bands packed into one message,
     one unpack on the root), run for n shards on one GPU with device copies in
-    place of RCCL: the root's u8 frame equals the unsharded frame byte for
+    place of RCCL: the root's frame output (u8 image, or its YUV420P planes:
+    a band's Y rows and its U and V rows) equals the unsharded frame byte for
     byte (odd widths take the byte-wise copy, multiples of 16 the vector one)."""
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    if fmt == "yuv420p" and (W % 2 or H % 2):
+        pytest.skip("YUV420P needs even sizes")
     xy, z, c = scenes.triangle_soup(2000, W, H, 18, seed=43, gouraud=True)
 
     def render(n, r):
         ctx = gpu.context(W, H, alpha)
+        ctx.set_frame_format(fmt)
         _set_shard(ctx, n, r, slots if n > 1 else None)
         ctx.set_color(0.2, 0.1, 0.3, 1.0)
         ctx.set_depth_state(True, True)
@@ -317,6 +323,8 @@ def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha,
     ref = render(1, 0)
     ref.gather_frame_u8()
     want = ref.get_frame_u8()
+    if fmt == "yuv420p":   # the raster's fused planes = the restatement of its u8 image
+        assert np.array_equal(want, scenes.yuv420p(ref.get_buffer_as_uint8_numpy()))
     ctxs = [render(nshards, r) for r in range(nshards)]
     R.RenderContext.gather_frame_u8_local(ctxs, root)
     got = ctxs[root].get_frame_u8()
@@ -351,14 +359,20 @@ def test_single_rank_comm_gather(gpu):
     assert np.array_equal(ctx.get_frame_u8(), ctx.get_buffer_as_uint8_numpy())
 
 
-def test_fused_frame_output_matches_conversion(gpu):
-    """After the first GatherFrameU8 the resolve writes the u8 frame itself;
-    the mirror must equal GetBufferAsUInt8 every frame, including frames with
-    a second (non-clearing) batch or a primitive drawn after the triangles."""
+@pytest.mark.parametrize("fmt", ["rgb", "yuv420p"])
+@pytest.mark.parametrize("alpha", [False, True])
+def test_fused_frame_output_matches_conversion(gpu, fmt, alpha):
+    """After the first GatherFrameU8 the resolve writes the frame output
+    itself (u8 image, or its YUV420P planes); it must equal GetBufferAsUInt8
+    (resp. the YUV420P restatement of it) every frame, including frames with a
+    second (non-clearing) batch, a primitive drawn after the triangles, or a
+    blended batch (ordered raster: converted after it)."""
     W, H = 300, 200
     xy, z, c = scenes.triangle_soup(2000, W, H, 15, seed=51, gouraud=True)
-    ctx = gpu.context(W, H, False)
-    for frame in range(4):
+    ctx = gpu.context(W, H, alpha)
+    ctx.set_frame_format(fmt)
+    conv = (lambda a: a) if fmt == "rgb" else scenes.yuv420p
+    for frame in range(5):
         ctx.set_color(0.05 * frame, 0.05 * frame, 0.05 * frame, 0.05 * frame)
         ctx.set_depth_state(True, True)
         ctx.clear_depth()
@@ -367,8 +381,12 @@ def test_fused_frame_output_matches_conversion(gpu):
             ctx.draw_triangles(xy[:100] + 7.0, c[:100], z=z[:100] * 0.5)
         if frame == 3:
             ctx.draw_rect(20, 20, 50, 40, 1, 0, 0, 0.5)
+        if frame == 4:
+            cb = c.copy()
+            cb[:, 3::4] = 0.5
+            ctx.draw_triangles(xy[:300], cb[:300], z=z[:300])
         ctx.gather_frame_u8()
-        assert np.array_equal(ctx.get_frame_u8(), ctx.get_buffer_as_uint8_numpy()), frame
+        assert np.array_equal(ctx.get_frame_u8(), conv(ctx.get_buffer_as_uint8_numpy())), frame
 
 
 def test_pair_list_overflow_is_rerun_in_order(gpu, oracle):
