@@ -147,6 +147,16 @@ struct Texture {
     int device = 0;
 };
 
+// Binning geometry of a draw: the positions' transform, the frame and the
+// owned tile rows.  The same buffer binned under the same key gives the same
+// (tile, triangle) pairs, work items and dense tiles.
+struct BinKey {
+    f64 m[6];
+    i64 W, H;
+    int period;
+    u64 mask;
+};
+
 struct TriangleBuffer {
     i64 n = 0;
     bool gouraud = false;
@@ -155,6 +165,11 @@ struct TriangleBuffer {
     f64* rgba = nullptr;  // n*4 (flat) or n*12 (Gouraud)
     bool opaque = false;  // every vertex alpha == 1 (known at upload)
     int device = 0;
+    // totals of the last validated binning of this buffer (nr_tri_free.hip):
+    // a draw under the same key is sized from them and needs no validation
+    bool known = false;
+    BinKey knownKey;
+    u32 knownPairs = 0, knownHeavy = 0;
 };
 
 // host helpers shared across translation units

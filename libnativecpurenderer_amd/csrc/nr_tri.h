@@ -264,10 +264,12 @@ void finish_batch(RenderContext* ctx, const FrameParams& fp);
 
 // the two rasterisers (host side)
 void draw_ordered(RenderContext* ctx, const TriSrc& src);
-// immutable: binning may overlap the previous raster; callerOwned: the arrays
-// are the caller's device memory (DrawTrianglesDevice), so the batch is sized
-// exactly in the call -- an overflow re-run never reads them after it returns
-void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable, bool callerOwned);
+// tb: the batch is that (immutable) TriangleBuffer, so its binning may overlap
+// the previous raster and a repeat draw is sized from its known totals;
+// callerOwned: the arrays are the caller's device memory (DrawTrianglesDevice),
+// so the batch is sized exactly in the call -- an overflow re-run never reads
+// them after it returns
+void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned);
 void settle(RenderContext* ctx);
 
 }  // namespace nrtri

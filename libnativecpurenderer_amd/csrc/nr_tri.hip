@@ -116,7 +116,7 @@ Opacity device_opacity(RenderContext* ctx, const TriSrc& src) {
 }
 
 void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud, Opacity opq,
-          bool immutable = false, bool callerOwned = false) {
+          TriangleBuffer* tb = nullptr, bool callerOwned = false) {
     NR_CHECK(hipSetDevice(ctx->device));
     settle(ctx);
     if (n <= 0 || ctx->width <= 0 || ctx->height <= 0) return;
@@ -124,7 +124,7 @@ void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 
     TriSrc src{xy, z, rgba, gouraud ? 1 : 0, n};
     const bool freeEligible = ctx->ct[3] == 1 && ctx->forceOrdered == 0;
     if (freeEligible && opq == OPQ_UNKNOWN) opq = device_opacity(ctx, src);
-    if (freeEligible && opq == OPQ_OPAQUE) draw_free(ctx, src, immutable, callerOwned);
+    if (freeEligible && opq == OPQ_OPAQUE) draw_free(ctx, src, tb, callerOwned);
     else draw_ordered(ctx, src);
 }
 
@@ -184,10 +184,10 @@ void DrawTrianglesDevice(RenderContext* ctx, const f64* xy, const f64* z, const 
         f64* dc = dz + zn;
         NR_CHECK(hipMemcpyAsync(dxy, xy, (size_t)n * 6 * sizeof(f64), hipMemcpyDeviceToDevice, ctx->stream));
         NR_CHECK(hipMemcpyAsync(dc, rgba, (size_t)n * ncol * sizeof(f64), hipMemcpyDeviceToDevice, ctx->stream));
-        draw(ctx, dxy, z, dc, n, gouraud, OPQ_UNKNOWN, false, z != nullptr);   // z stays the caller's
+        draw(ctx, dxy, z, dc, n, gouraud, OPQ_UNKNOWN, nullptr, z != nullptr);   // z stays the caller's
         return;
     }
-    draw(ctx, xy, z, rgba, n, gouraud, OPQ_UNKNOWN, false, true);
+    draw(ctx, xy, z, rgba, n, gouraud, OPQ_UNKNOWN, nullptr, true);
 }
 
 // New: triangles from host arrays (copied to HBM first).
@@ -251,7 +251,7 @@ i64 GetTriangleBufferCount(TriangleBuffer* tb) { return tb->n; }
 
 void DrawTriangleBuffer(RenderContext* ctx, TriangleBuffer* tb) {
     // a TriangleBuffer never changes: its binning may overlap the previous batch's raster
-    draw(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud, tb->opaque ? OPQ_OPAQUE : OPQ_BLENDED, true);
+    draw(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud, tb->opaque ? OPQ_OPAQUE : OPQ_BLENDED, tb);
 }
 
 // New: count covered on-screen pixel x triangle pairs (the "shaded+Z-tested

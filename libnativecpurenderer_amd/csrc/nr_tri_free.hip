@@ -32,6 +32,7 @@
 #include <hip/hip_ext.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 
 namespace nrtri {
@@ -73,16 +74,26 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
                                                     u64* __restrict__ rects) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
+    const i64 base = (i64)blockIdx.x * 256 * TPT;
+    // every triangle's positions first (in flight during the histogram's
+    // zeroing): one round of load latency, not TPT
+    f64 pxy[TPT][6];
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
+    }
     if (LDSH) {
         for (int b = tid; b < ntiles; b += 256) hist[b] = 0;
         __syncthreads();
     }
-    const i64 base = (i64)blockIdx.x * 256 * TPT;
+#pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
         if (t >= bp.src.n) break;
         f64 sx[3], sy[3];
-        tri_screen(bp.src, bp.m, t, sx, sy);
+#pragma unroll
+        for (int v = 0; v < 3; ++v) nr_xform(bp.m, pxy[k][2 * v], pxy[k][2 * v + 1], sx[v], sy[v]);
         int tx0, tx1, ty0, ty1;
         const bool hit = tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1);
         rects[t] = hit ? pack_rect(tx0, tx1, ty0, ty1) : NO_RECT;
@@ -357,6 +368,118 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
     }
 }
 
+// The same plan with every tile count read once, into registers: thread t
+// owns the PR = ceil(ntiles / T) <= 16 consecutive tiles [t*PR, t*PR + PR), so
+// the kernel makes one round of global loads instead of one per pass and per
+// block of tiles (its duration is latency: the two kernels above made 12 and
+// 3 dependent rounds), then three workgroup barriers.  Used whenever ntiles <=
+// 16 * T (T = 1024: 16384 tiles, an 8K frame; T = 256: 4096, a 4K frame).
+constexpr int PR_MAX = 16;
+template <int T>
+__global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
+                                                   u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
+                                                   u32* __restrict__ cur, u32* __restrict__ totals,
+                                                   u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
+                                                   u32 slice_target) {
+    constexpr int NWV = T / 64;
+    __shared__ u32 sh[4][NWV];
+    __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < PLAN_NB) bcnt[tid] = 0;
+    const int per = (ntiles + T - 1) / T;
+    const int i0 = tid * per;
+    u32 c[PR_MAX];
+#pragma unroll
+    for (int j = 0; j < PR_MAX; ++j) c[j] = (j < per && i0 + j < ntiles) ? cnt[i0 + j] : 0u;
+    u32 a = 0, hv = 0;
+#pragma unroll
+    for (int j = 0; j < PR_MAX; ++j) {
+        a += c[j];
+        hv += c[j] >= HEAVY_PAIRS ? 1u : 0u;
+    }
+    const u32 ia = wave_scan(a, lane), ih = wave_scan(hv, lane);
+    if (lane == 63) { sh[0][w] = ia; sh[1][w] = ih; }
+    __syncthreads();
+    u32 ta = 0, th = 0, ea = ia - a;   // ea: list offset of this thread's first tile
+#pragma unroll
+    for (int k = 0; k < NWV; ++k) {
+        if (k < w) ea += sh[0][k];
+        ta += sh[0][k];
+        th += sh[1][k];
+    }
+    u32 slice = SLICE_MIN;
+    while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
+    // items per tile and per size class (ownership: tile row of i0 + j)
+    const int ty0 = i0 / tiles_x, tx0 = i0 - ty0 * tiles_x;
+    u32 b = 0, m = 0;
+    {
+        int ty = ty0, tx = tx0;
+#pragma unroll
+        for (int j = 0; j < PR_MAX; ++j) {
+            if (j < per && i0 + j < ntiles) {
+                const u32 ni = tile_items(c[j], owned_row(ty, period, mask), slice);
+                b += ni;
+                m += c[j] > slice ? 1u : 0u;
+                if (ni) atomicAdd(&bcnt[size_class(c[j], slice)], ni);
+            }
+            if (++tx == tiles_x) { tx = 0; ++ty; }
+        }
+    }
+    const u32 ib = wave_scan(b, lane), im = wave_scan(m, lane);
+    if (lane == 63) { sh[2][w] = ib; sh[3][w] = im; }
+    __syncthreads();
+    u32 tb = 0, tm = 0;
+#pragma unroll
+    for (int k = 0; k < NWV; ++k) { tb += sh[2][k]; tm += sh[3][k]; }
+    const bool fits = ta <= cap && tb <= icap;
+    if (tid == 0) {   // item ranges of the classes, largest class first
+        u32 base = 0;
+        for (int k = PLAN_NB - 1; k >= 0; --k) { bcur[k] = base; base += bcnt[k]; }
+    }
+    __syncthreads();
+    {
+        int ty = ty0, tx = tx0;
+#pragma unroll
+        for (int j = 0; j < PR_MAX; ++j) {
+            const int i = i0 + j;
+            if (j < per && i < ntiles) {
+                off[i] = ea;
+                const u32 ni = tile_items(c[j], owned_row(ty, period, mask), slice);
+                if (fits && ni) {
+                    const u32 eb = atomicAdd(&bcur[size_class(c[j], slice)], ni);
+                    for (u32 k = 0; k < ni; ++k) {
+                        const u32 ls = ea + k * slice;
+                        items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + c[j]), ni);
+                    }
+                }
+                cnt[i] = 0;
+                cur[i] = 0;
+                ea += c[j];
+            }
+            if (++tx == tiles_x) { tx = 0; ++ty; }
+        }
+    }
+    if (tid == 0) {
+        off[ntiles] = ta;
+        const u32 t[4] = {ta, tb, tm, fits ? 1u : 0u};
+        for (int k = 0; k < 4; ++k) {
+            totals[k] = t[k];
+            __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// NR_PLAN_REG=0 keeps the multi-round plan kernels (A/B).
+static bool plan_reg() {
+    static const bool v = [] {
+        const char* e = getenv("NR_PLAN_REG");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // Which plan kernel: the 256-thread one when the batch's owned share is large
 // (>= 2^17 triangles' worth: C3 unsharded 0.167 -> 0.160 ms per frame, C3 4-way
 // share 0.0654 -> 0.0627 ms; the plan runs beside the previous, long k_vis),
@@ -382,13 +505,19 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
     if (!plan[3]) return;
     const int tid = threadIdx.x;
     const i64 base = (i64)blockIdx.x * 256 * TPT;
+    u64 rk[TPT];   // every rectangle first: one round of load latency
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        rk[k] = t < bp.src.n ? rects[t] : NO_RECT;
+    }
     if (LDSH) {
         for (int b = tid; b < ntiles; b += 256) hist[b] = 0;
         __syncthreads();
         for (int k = 0; k < TPT; ++k) {
             const i64 t = base + k * 256 + tid;
             if (t >= bp.src.n) break;
-            const u64 rc = rects[t];
+            const u64 rc = rk[k];
             if (rc == NO_RECT) continue;
             const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
             const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
@@ -407,7 +536,7 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
         if (t >= bp.src.n) break;
-        const u64 rc = rects[t];
+        const u64 rc = rk[k];
         if (rc == NO_RECT) continue;
         const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
         const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
@@ -884,12 +1013,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
         // back the whole L2): the keys only ever move through device-scope
         // atomics and sc1 loads/stores, each wave drains its atomics before
         // the barrier, and the slice counter is a relaxed device atomic.
+        // Only keys this slice changed are merged: a key still at its initial
+        // value has no triangle id in its low word (ids are t + 1 >= 1), and the
+        // initial value never beats another slice's key; a pixel no slice
+        // changed keeps the neutral global key, read back below as "no winner".
         for (int p = tid; p < TH * TW; p += NT) {
             const int lx = p & (TW - 1), ly = p / TW;
             if (lx >= wlim || ly >= hlim) continue;
+            const u64 kk = key[ly * KS + lx];
+            if (!(u32)kk) continue;
             u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-            if (ZMODE == 1) atomicMin(g, key[ly * KS + lx]);
-            else atomicMax(g, key[ly * KS + lx]);
+            if (ZMODE == 1) atomicMin(g, kk);
+            else atomicMax(g, kk);
         }
         __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: this wave's atomics performed
         __syncthreads();
@@ -905,8 +1040,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
             const int lx = p & (TW - 1), ly = p / TW;
             if (lx >= wlim || ly >= hlim) continue;
             u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-            key[ly * KS + lx] = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(g, ZMODE == 1 ? ~0ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u64 neutral = ZMODE == 1 ? ~0ull : 0ull;
+            const u64 gv = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            key[ly * KS + lx] = gv == neutral ? 0ull : gv;   // untouched: no winner (only the id word is read)
+            if (gv != neutral) __hip_atomic_store(g, neutral, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         shade_tile<ZMODE, GOURAUD, NT>(fp, x0, y0, wlim, hlim, key, lds, nU);
@@ -986,7 +1123,25 @@ struct PendingBatch {
     BinParams bp;
     int set;
     u32 seq;
+    TriangleBuffer* tb;   // non-null: record the validated totals as its known sizes
+    BinKey key;
 };
+
+static BinKey bin_key(const BinParams& bp) {
+    BinKey k;
+    memset(&k, 0, sizeof k);   // padding too: keys are compared bytewise
+    for (int i = 0; i < 6; ++i) k.m[i] = bp.m[i];
+    k.W = bp.W; k.H = bp.H; k.period = bp.period; k.mask = bp.mask;
+    return k;
+}
+
+static void record_known(TriangleBuffer* tb, const BinKey& key, u32 pairs, u32 heavy) {
+    if (!tb) return;
+    tb->known = true;
+    tb->knownKey = key;
+    tb->knownPairs = pairs;
+    tb->knownHeavy = heavy;
+}
 
 // Items the plan kernel aims for when it picks the slice length
 // (NR_SLICE_TARGET; the environment variable of the same name overrides it).
@@ -1024,7 +1179,7 @@ static hipEvent_t sync_event() {
 // queued before on the main stream -- so that it overlaps the previous
 // batch's k_vis (only for immutable inputs: a TriangleBuffer).
 static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
-                         bool exact, int si, bool pipelined, u32* seqOut) {
+                         bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0) {
     hipStream_t sa = ctx->stream;
     hipStream_t sb = pipelined ? nr_bin_stream_for(ctx->device) : sa;
     TriScratch& sc = ctx->tri;
@@ -1094,7 +1249,8 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     F.frect = rb[0];
     size_t cap;
     if (!exact) {
-        const u64 est = std::max<u64>(std::max<u64>(sc.lastPairs + sc.lastPairs / 4, (u64)src.n * 2), 1u << 20);
+        const u64 est = std::max<u64>(std::max<u64>(std::max<u64>(sc.lastPairs + sc.lastPairs / 4, (u64)src.n * 2), 1u << 20),
+                                      knownPairs);
         cap = (size_t)std::min<u64>(sc.capOverride ? sc.capOverride : est, 0xFFFFFFF0ull);
         if (!grow_list(cap)) return false;
         if (!sc.capOverride) cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
@@ -1120,7 +1276,20 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        if (plan_small(fp.period, fp.mask, src.n))
+        const bool small = plan_small(fp.period, fp.mask, src.n);
+        const u32 icap32 = (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull);
+        // the register plan: 256 threads whenever the tiles fit (one wave per
+        // SIMD, 86 VGPRs: it fits beside running k_vis workgroups, where the
+        // 1024-thread one waits for a whole CU to drain)
+        if (plan_reg() && ntiles <= PS_T * PR_MAX)
+            hipLaunchKernelGGL(k_free_plan_r<PS_T>, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
+                               fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap, icap32, seq,
+                               slice_target());
+        else if (plan_reg() && !small && ntiles <= PLAN_T * PR_MAX)
+            hipLaunchKernelGGL(k_free_plan_r<PLAN_T>, dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, fp.tiles_x,
+                               fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap, icap32, seq,
+                               slice_target());
+        else if (small)
             hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
                                (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
@@ -1181,7 +1350,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
 
 }  // namespace
 
-void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable, bool callerOwned) {
+void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned) {
     FrameParams fp = frame_params(ctx, src);
     if (ctx->frameOutput && fp.pendColor) {
         const size_t n = (size_t)nr_frame_bytes(ctx);
@@ -1198,12 +1367,36 @@ void draw_free(RenderContext* ctx, const TriSrc& src, bool immutable, bool calle
     // synchronised and released or rewritten them
     const bool exact = fp.fragCounter != nullptr || callerOwned;
     TriScratch& sc = ctx->tri;
+    // A TriangleBuffer drawn again under the binning key of its last validated
+    // draw has the same pair total: the list is sized to hold it, so the plan's
+    // capacity check cannot fail and the batch needs no validation (no host
+    // wait for its plan kernel at the next call: the host runs ahead).
+    const BinKey key = bin_key(bp);
+    // Only unsharded batches: a sharded frame's raster is short, and a binning
+    // chain issued at once runs beside it and is starved (measured: 1 GPU C3
+    // 0.1640 -> 0.1614 ms, C2 0.0685 -> 0.062 ms with known sizes; an emulated
+    // rank share of 4 / 8 shards 0.066 -> 0.076 / 0.054 -> 0.062 ms, where the
+    // host wait on the plan paces the binning; profiles/r02_c3/ab_known.txt).
+    // NR_KNOWN_SIZES=0 / 2: never / also for sharded batches (A/B).
+    static const int knownMode = [] {
+        const char* e = getenv("NR_KNOWN_SIZES");
+        return e ? atoi(e) : 1;
+    }();
+    const bool known = knownMode != 0 && (fp.period == 1 || knownMode == 2) && tb && tb->known && !sc.capOverride &&
+                       memcmp(&tb->knownKey, &key, sizeof key) == 0;
+    if (known && !exact) {   // this batch's totals pick the k_vis variant (launch_vis)
+        sc.lastN = (u64)src.n;
+        sc.lastPairs = tb->knownPairs;
+        sc.lastHeavy = tb->knownHeavy;
+    }
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % bin_sets();
     u32 seq = 0;
-    if (!free_enqueue(ctx, src, fp, bp, exact, si, immutable && !exact, &seq)) return;
-    if (!exact) {
-        PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq};
+    if (!free_enqueue(ctx, src, fp, bp, exact, si, tb != nullptr && !exact, &seq, known ? tb->knownPairs : 0)) return;
+    if (exact) {
+        record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy);
+    } else if (!known) {
+        PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq, tb, key};
         ctx->pendingBatch = pb;
     }
     ctx->lastPath = 1;
@@ -1241,6 +1434,7 @@ void settle(RenderContext* ctx) {
     sc.lastN = (u64)pb->src.n;
     sc.lastPairs = F.h_plan[0];
     sc.lastHeavy = F.h_plan[5];
+    record_known(pb->tb, pb->key, F.h_plan[0], F.h_plan[5]);   // exact totals, whether or not they fitted
     if (!F.h_plan[3]) {
         // overflow: the batch's later kernels did nothing; re-run it exactly
         // on the main stream, after everything queued so far

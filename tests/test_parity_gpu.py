@@ -145,6 +145,42 @@ def test_triangle_buffer_equals_host_arrays(gpu):
     assert_same(a, {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, "buffer")
 
 
+def test_triangle_buffer_repeat_draws_sized_from_known_totals(gpu):
+    """A TriangleBuffer drawn again under the binning key (transform, frame,
+    shard) of its last validated draw is sized from the recorded totals and
+    not validated on the host.  Alternate keys (transforms, sizes, shards) and
+    repeats: every frame equals the same draw from host arrays (validated)."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    xy, z, c = scenes.triangle_soup(6000, 420, 300, 16, seed=71, gouraud=True)
+    buf = R.TriangleBuffer(xy, c, z=z)
+    states = [((0, 0), 420, 300, None), ((0, 0), 420, 300, None), ((7.5, -3.25), 420, 300, None),
+              ((0, 0), 420, 300, None), ((0, 0), 400, 300, None), ((0, 0), 420, 300, (3, 1)),
+              ((0, 0), 420, 300, (3, 1)), ((0, 0), 420, 300, None), ((7.5, -3.25), 420, 300, None)]
+    ctxs = {}
+    for i, (t, W, H, shard) in enumerate(states):
+        outs = []
+        for use_buf in (True, False):
+            key = (W, H, use_buf)
+            if key not in ctxs:
+                ctxs[key] = gpu.context(W, H, False)
+            ctx = ctxs[key]
+            if shard is None:
+                ctx.set_shard(1, 0)
+            else:
+                ctx.set_shard(*shard)
+            ctx.set_transform(1, 0, 0, 1, *t)
+            ctx.set_color(0.1, 0.1, 0.1, 0.1)
+            ctx.set_depth_state(True, True)
+            ctx.clear_depth()
+            if use_buf:
+                ctx.draw_triangle_buffer(buf)
+            else:
+                ctx.draw_triangles(xy, c, z=z)
+            ctx.gather_frame_u8()
+            outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer(), "u8": ctx.get_frame_u8()})
+        assert_same(outs[0], outs[1], f"repeat {i}")
+
+
 @pytest.mark.parametrize("misalign", [False, True])
 def test_device_arrays_match_oracle(gpu, oracle, misalign):
     """DrawTrianglesDevice on torch HBM tensors, 16-byte aligned or not
