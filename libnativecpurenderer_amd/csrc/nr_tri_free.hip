@@ -127,16 +127,22 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
 // and the emit cursors, and mirrors the totals into pinned host memory, so a
 // batch needs no memset and no copy command.
 __device__ __forceinline__ u32 tile_items(u32 c, bool owned, u32 slice) {
-    return owned ? (c > slice ? (c + slice - 1) / slice : 1u) : 0u;
+    // slice is a power of two: the division is a shift
+    return owned ? (c > slice ? (c + slice - 1) >> (31 - __clz(slice)) : 1u) : 0u;
 }
 
-// Inclusive wave scan (64 lanes).
-__device__ __forceinline__ u32 wave_scan(u32 v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const u32 o = __shfl_up(v, d, 64);
-        if (lane >= d) v += o;
-    }
+// Inclusive wave scan (64 lanes) with DPP row shifts and row broadcasts
+// (VALU, a few cycles per step): Hillis-Steele inside each row of 16 lanes,
+// then row 0's total into row 1 and row 2's into row 3 (row_bcast:15), then
+// row 1's into rows 2 and 3 (row_bcast:31).  The __shfl_up form is a chain of
+// six dependent LDS permutes (~100+ cycles each).
+__device__ __forceinline__ u32 wave_scan(u32 v, int) {
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
     return v;
 }
 
@@ -369,13 +375,19 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
 }
 
 // The same plan with every tile count read once, into registers: thread t
-// owns the PR = ceil(ntiles / T) <= 16 consecutive tiles [t*PR, t*PR + PR), so
+// owns PR = 4 * ceil(ntiles / 4T) <= 16 consecutive tiles [t*PR, t*PR + PR), read and
+// written as 16-byte vectors (the tile arrays are allocated to TILE_ARR entries,
+// so the padding past ntiles -- never counted, so zero -- is in bounds), so
 // the kernel makes one round of global loads instead of one per pass and per
-// block of tiles (its duration is latency: the two kernels above made 12 and
-// 3 dependent rounds), then three workgroup barriers.  Used whenever ntiles <=
-// 16 * T (T = 1024: 16384 tiles, an 8K frame; T = 256: 4096, a 4K frame).
+// block of tiles.  Items are placed by size class without same-address LDS
+// atomics (a wave's lanes mostly share a class, and such atomics serialise):
+// per-lane class counts in registers, per-class wave scans, one LDS slot per
+// (class, wave).  Used whenever ntiles <= 16 * T (T = 256: 4096 tiles, a 4K
+// frame; T = 1024: 16384, an 8K frame).  Measured alone on C3 (rocprof): the
+// first register version 16 us, this one see DESIGN.md §4.
 constexpr int PR_MAX = 16;
-template <int T>
+constexpr int TILE_ARR = 16 * 1024 + 4;   // minimum length of the per-tile arrays
+template <int T, int PR>
 __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
                                                    u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                    u32* __restrict__ cur, u32* __restrict__ totals,
@@ -383,17 +395,20 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
                                                    u32 slice_target) {
     constexpr int NWV = T / 64;
     __shared__ u32 sh[4][NWV];
-    __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
+    __shared__ u32 csh[PLAN_NB][NWV];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid < PLAN_NB) bcnt[tid] = 0;
-    const int per = (ntiles + T - 1) / T;
+    const int per = (((ntiles + T - 1) / T) + 3) & ~3;
     const int i0 = tid * per;
-    u32 c[PR_MAX];
+    u32 c[PR];
 #pragma unroll
-    for (int j = 0; j < PR_MAX; ++j) c[j] = (j < per && i0 + j < ntiles) ? cnt[i0 + j] : 0u;
+    for (int q = 0; q < PR / 4; ++q) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (4 * q < per) v = reinterpret_cast<const uint4*>(cnt + i0)[q];
+        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+    }
     u32 a = 0, hv = 0;
 #pragma unroll
-    for (int j = 0; j < PR_MAX; ++j) {
+    for (int j = 0; j < PR; ++j) {
         a += c[j];
         hv += c[j] >= HEAVY_PAIRS ? 1u : 0u;
     }
@@ -409,21 +424,30 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     }
     u32 slice = SLICE_MIN;
     while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
-    // items per tile and per size class (ownership: tile row of i0 + j)
+    // items per tile, per-lane totals per size class (ownership: tile row of i0 + j)
     const int ty0 = i0 / tiles_x, tx0 = i0 - ty0 * tiles_x;
-    u32 b = 0, m = 0;
+    u32 b = 0, m = 0, hc[PLAN_NB];
+#pragma unroll
+    for (int k = 0; k < PLAN_NB; ++k) hc[k] = 0;
     {
         int ty = ty0, tx = tx0;
 #pragma unroll
-        for (int j = 0; j < PR_MAX; ++j) {
-            if (j < per && i0 + j < ntiles) {
-                const u32 ni = tile_items(c[j], owned_row(ty, period, mask), slice);
-                b += ni;
-                m += c[j] > slice ? 1u : 0u;
-                if (ni) atomicAdd(&bcnt[size_class(c[j], slice)], ni);
-            }
+        for (int j = 0; j < PR; ++j) {
+            const u32 ni = (j < per && i0 + j < ntiles) ? tile_items(c[j], owned_row(ty, period, mask), slice) : 0u;
+            b += ni;
+            m += c[j] > slice ? 1u : 0u;
+            const int cls = size_class(c[j], slice);
+#pragma unroll
+            for (int k = 0; k < PLAN_NB; ++k) hc[k] += cls == k ? ni : 0u;
             if (++tx == tiles_x) { tx = 0; ++ty; }
         }
+    }
+    // per class: this lane's exclusive position among the wave's items
+#pragma unroll
+    for (int k = 0; k < PLAN_NB; ++k) {
+        const u32 inc = wave_scan(hc[k], lane);
+        if (lane == 63) csh[k][w] = inc;
+        hc[k] = inc - hc[k];
     }
     const u32 ib = wave_scan(b, lane), im = wave_scan(m, lane);
     if (lane == 63) { sh[2][w] = ib; sh[3][w] = im; }
@@ -432,35 +456,54 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
 #pragma unroll
     for (int k = 0; k < NWV; ++k) { tb += sh[2][k]; tm += sh[3][k]; }
     const bool fits = ta <= cap && tb <= icap;
-    if (tid == 0) {   // item ranges of the classes, largest class first
-        u32 base = 0;
-        for (int k = PLAN_NB - 1; k >= 0; --k) { bcur[k] = base; base += bcnt[k]; }
+    // class ranges, largest class first, and each wave's base inside them:
+    // thread k < PLAN_NB turns column k of csh into the wave bases of class k
+    if (tid < PLAN_NB) {
+        u32 start = 0;
+        for (int k = PLAN_NB - 1; k > tid; --k)
+            for (int q = 0; q < NWV; ++q) start += csh[k][q];
+        for (int q = 0; q < NWV; ++q) {
+            const u32 v = csh[tid][q];
+            csh[tid][q] = start;
+            start += v;
+        }
     }
     __syncthreads();
-    {
+#pragma unroll
+    for (int k = 0; k < PLAN_NB; ++k) hc[k] += csh[k][w];
+    {   // c[j] becomes tile j's list offset
         int ty = ty0, tx = tx0;
 #pragma unroll
-        for (int j = 0; j < PR_MAX; ++j) {
+        for (int j = 0; j < PR; ++j) {
+            const u32 cj = c[j];
+            c[j] = ea;
             const int i = i0 + j;
-            if (j < per && i < ntiles) {
-                off[i] = ea;
-                const u32 ni = tile_items(c[j], owned_row(ty, period, mask), slice);
-                if (fits && ni) {
-                    const u32 eb = atomicAdd(&bcur[size_class(c[j], slice)], ni);
-                    for (u32 k = 0; k < ni; ++k) {
-                        const u32 ls = ea + k * slice;
-                        items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + c[j]), ni);
-                    }
+            const u32 ni = (j < per && i < ntiles) ? tile_items(cj, owned_row(ty, period, mask), slice) : 0u;
+            const int cls = size_class(cj, slice);
+            u32 eb = 0;
+#pragma unroll
+            for (int k = 0; k < PLAN_NB; ++k)
+                if (cls == k) { eb = hc[k]; hc[k] += ni; }
+            if (fits)
+                for (u32 k = 0; k < ni; ++k) {
+                    const u32 ls = ea + k * slice;
+                    items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + cj), ni);
                 }
-                cnt[i] = 0;
-                cur[i] = 0;
-                ea += c[j];
-            }
+            ea += cj;
             if (++tx == tiles_x) { tx = 0; ++ty; }
         }
     }
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int q = 0; q < PR / 4; ++q) {
+        if (4 * q < per) {
+            reinterpret_cast<uint4*>(off + i0)[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
+            reinterpret_cast<uint4*>(cnt + i0)[q] = z4;
+            reinterpret_cast<uint4*>(cur + i0)[q] = z4;
+        }
+    }
     if (tid == 0) {
-        off[ntiles] = ta;
+        off[ntiles] = ta;   // (the same value as the padding stores write there)
         const u32 t[4] = {ta, tb, tm, fits ? 1u : 0u};
         for (int k = 0; k < 4; ++k) {
             totals[k] = t[k];
@@ -1195,10 +1238,11 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         if (F.visRecorded) NR_CHECK(hipEventSynchronize(F.evVis));
     };
 
-    if (F.ftile_cap < (size_t)ntiles + 1 || !F.fcnt) quiesce();
+    if (F.ftile_cap < std::max<size_t>((size_t)ntiles + 1, TILE_ARR) || !F.fcnt) quiesce();
     u32* tb[3] = {F.fcnt, F.foff, F.fcur};
     const size_t oldcap = F.ftile_cap;
-    if (!grow_set(tb, &F.ftile_cap, (size_t)ntiles + 1)) return false;
+    // (k_free_plan_r reads and writes the tile arrays as 16-byte vectors up to TILE_ARR)
+    if (!grow_set(tb, &F.ftile_cap, std::max<size_t>((size_t)ntiles + 1, TILE_ARR))) return false;
     F.fcnt = tb[0]; F.foff = tb[1]; F.fcur = tb[2];
     if (F.ftile_cap != oldcap) {   // counters start at zero; k_free_plan re-zeroes them after each use
         NR_CHECK(hipMemsetAsync(F.fcnt, 0, F.ftile_cap * sizeof(u32), sb));
@@ -1281,14 +1325,18 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         // the register plan: 256 threads whenever the tiles fit (one wave per
         // SIMD, 86 VGPRs: it fits beside running k_vis workgroups, where the
         // 1024-thread one waits for a whole CU to drain)
-        if (plan_reg() && ntiles <= PS_T * PR_MAX)
-            hipLaunchKernelGGL(k_free_plan_r<PS_T>, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
-                               fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap, icap32, seq,
-                               slice_target());
-        else if (plan_reg() && !small && ntiles <= PLAN_T * PR_MAX)
-            hipLaunchKernelGGL(k_free_plan_r<PLAN_T>, dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, fp.tiles_x,
-                               fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap, icap32, seq,
-                               slice_target());
+        if (plan_reg() && !small && ntiles <= PLAN_T * PR_MAX) {
+            // 1024 threads, PR = tiles per thread -> 4, 8 or 16.  Beside a long
+            // raster (small) the 65-VGPR multi-round k_free_plan_s stays: it fits the
+            // slot a finishing k_vis workgroup frees, the register plan (>128 VGPRs
+            // at PR 16) does not (C3 0.163 vs 0.172 ms; profiles/r02_c3/ab_plan_r.txt)
+            const int per = (ntiles + PLAN_T - 1) / PLAN_T;
+#define NR_PLAN_R(PP) hipLaunchKernelGGL((k_free_plan_r<PLAN_T, PP>), dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, \
+                                         fp.tiles_x, fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, \
+                                         (u32)cap, icap32, seq, slice_target())
+            if (per <= 4) NR_PLAN_R(4); else if (per <= 8) NR_PLAN_R(8); else NR_PLAN_R(16);
+#undef NR_PLAN_R
+        }
         else if (small)
             hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
@@ -1392,7 +1440,13 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % bin_sets();
     u32 seq = 0;
-    if (!free_enqueue(ctx, src, fp, bp, exact, si, tb != nullptr && !exact, &seq, known ? tb->knownPairs : 0)) return;
+    static const bool pipeOn = [] {   // NR_BIN_PIPE=0: bin on the main stream (A/B, isolated kernel times)
+        const char* e = getenv("NR_BIN_PIPE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    if (!free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact, &seq,
+                      known ? tb->knownPairs : 0))
+        return;
     if (exact) {
         record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy);
     } else if (!known) {

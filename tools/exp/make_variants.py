@@ -21,10 +21,26 @@ VARIANTS = {
     "nst": ["EXP_NOF64ST", "EXP_NOU8ST"],
     "plant": ["EXP_PLANT"],
     "times": ["EXP_TIMES"],
+    "planr": ["EXP_PLANR"],
     "sht": ["EXP_SHT"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
 PATCHES = {
+    "EXP_PLANR": [   # s_memrealtime stamps at k_free_plan_r's phase boundaries -> g_exp[8*slot + 0..5]
+        ("    const int per = (((ntiles + T - 1) / T) + 3) & ~3;\n",
+         "    const u64 pr0 = __builtin_amdgcn_s_memrealtime();\n    const int per = (((ntiles + T - 1) / T) + 3) & ~3;\n"),
+        ("    const u32 ia = wave_scan(a, lane), ih = wave_scan(hv, lane);\n",
+         "    __builtin_amdgcn_s_waitcnt(0);\n    const u64 pr1 = __builtin_amdgcn_s_memrealtime();\n    const u32 ia = wave_scan(a, lane), ih = wave_scan(hv, lane);\n"),
+        ("    const u32 ib = wave_scan(b, lane), im = wave_scan(m, lane);\n",
+         "    const u64 pr2 = __builtin_amdgcn_s_memrealtime();\n    const u32 ib = wave_scan(b, lane), im = wave_scan(m, lane);\n"),
+        ("    {   // c[j] becomes tile j's list offset\n",
+         "    const u64 pr3 = __builtin_amdgcn_s_memrealtime();\n    {   // c[j] becomes tile j's list offset\n"),
+        ("    if (tid == 0) {\n        off[ntiles] = ta;   // (the same",
+         "    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();\n    const u64 pr4 = __builtin_amdgcn_s_memrealtime();\n    if (tid == 0) {\n        off[ntiles] = ta;   // (the same"),
+        ("        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);\n    }\n}\n\n// NR_PLAN_REG",
+         "        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);\n"
+         "        __builtin_amdgcn_s_waitcnt(0);\n        const u64 pr5 = __builtin_amdgcn_s_memrealtime();\n        const u64 slot = atomicAdd(&g_acc[7], 1ull) % 4096;\n        g_exp[8 * slot] = pr0; g_exp[8 * slot + 1] = pr1; g_exp[8 * slot + 2] = pr2; g_exp[8 * slot + 3] = pr3; g_exp[8 * slot + 4] = pr4; g_exp[8 * slot + 5] = pr5; g_exp[8 * slot + 6] = T;\n    }\n}\n\n// NR_PLAN_REG"),
+    ],
     "EXP_TIMES": [
         ("    for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {\n",
          "    u64 exp_t0 = 0, exp_mid = 0; u32 exp_prev = ~0u; u64 exp_info = 0;\n"
