@@ -22,10 +22,23 @@ VARIANTS = {
     "plant": ["EXP_PLANT"],
     "times": ["EXP_TIMES"],
     "planr": ["EXP_PLANR"],
+    "binph": ["EXP_BINPH"],
     "sht": ["EXP_SHT"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
 PATCHES = {
+    "EXP_BINPH": [   # per-WG phase durations of k_free_count / k_free_emit -> g_acc[0..3] (count), g_acc[4..6] (emit), spans g_exp
+        ("    f64 pxy[TPT][6];\n#pragma unroll\n    for (int k = 0; k < TPT; ++k) {\n        const i64 t = base + k * 256 + tid;\n        if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);\n    }\n",
+         "    const u64 c_t0 = __builtin_amdgcn_s_memrealtime();\n    f64 pxy[TPT][6];\n#pragma unroll\n    for (int k = 0; k < TPT; ++k) {\n        const i64 t = base + k * 256 + tid;\n        if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);\n    }\n"
+         "    __builtin_amdgcn_s_waitcnt(0);\n    const u64 c_t1 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("    if (LDSH) {\n        for (int b = tid; b < ntiles; b += 256) hist[b] = 0;\n        __syncthreads();\n    }\n#pragma unroll\n",
+         "    if (LDSH) {\n        for (int b = tid; b < ntiles; b += 256) hist[b] = 0;\n        __syncthreads();\n    }\n    const u64 c_t2 = __builtin_amdgcn_s_memrealtime();\n#pragma unroll\n"),
+        ("    if (LDSH) {\n        __syncthreads();\n        for (int b = tid; b < ntiles; b += 256) {\n            const u32 h = hist[b];\n            if (h) atomicAdd(&tile_cnt[b], h);\n        }\n    }\n}",
+         "    if (LDSH) {\n        __syncthreads();\n        const u64 c_t3 = __builtin_amdgcn_s_memrealtime();\n        for (int b = tid; b < ntiles; b += 256) {\n            const u32 h = hist[b];\n            if (h) atomicAdd(&tile_cnt[b], h);\n        }\n"
+         "        __builtin_amdgcn_s_waitcnt(0);\n        __syncthreads();\n        if (tid == 0) { const u64 c_t4 = __builtin_amdgcn_s_memrealtime();\n"
+         "            atomicAdd(&g_acc[0], c_t1 - c_t0); atomicAdd(&g_acc[1], c_t2 - c_t1); atomicAdd(&g_acc[2], c_t3 - c_t2); atomicAdd(&g_acc[3], c_t4 - c_t3);\n"
+         "            atomicAdd(&g_acc[7], 1ull); atomicMin(&g_exp[0], c_t0); atomicMax(&g_exp[1], c_t4); }\n    }\n}"),
+    ],
     "EXP_PLANR": [   # s_memrealtime stamps at k_free_plan_r's phase boundaries -> g_exp[8*slot + 0..5]
         ("    const int per = (((ntiles + T - 1) / T) + 3) & ~3;\n",
          "    const u64 pr0 = __builtin_amdgcn_s_memrealtime();\n    const int per = (((ntiles + T - 1) / T) + 3) & ~3;\n"),
@@ -59,13 +72,13 @@ PATCHES = {
     "EXP_SHT": [   # shading phase durations summed over all shade_tile calls -> g_acc
         ("    for (int i = tid; i < HTS; i += NT) ht[i] = 0;\n",
          "    const u64 sh_t0 = __builtin_amdgcn_s_memrealtime();\n    for (int i = tid; i < HTS; i += NT) ht[i] = 0;\n"),
-        ("    __syncthreads();\n    // one record per staged winner",
-         "    __syncthreads();\n    const u64 sh_t1 = __builtin_amdgcn_s_memrealtime();\n    // one record per staged winner"),
+        ("    __syncthreads();   // every key read: the records may overwrite them\n",
+         "    __syncthreads();   // every key read: the records may overwrite them\n    const u64 sh_t1 = __builtin_amdgcn_s_memrealtime();\n"),
         ("    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    __syncthreads();\n",
          "    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    __syncthreads();\n"
          "    const u64 sh_t2 = __builtin_amdgcn_s_memrealtime();\n"),
-        ("        store_pixel<ZMODE>(fp, gp, kv, cr, cg, cb, ca);\n    }\n}",
-         "        store_pixel<ZMODE>(fp, gp, kv, cr, cg, cb, ca);\n    }\n    __syncthreads();\n"
+        ("        store_colour(fp, gp, px, py, cr, cg, cb, ca);\n    }\n}",
+         "        store_colour(fp, gp, px, py, cr, cg, cb, ca);\n    }\n    __syncthreads();\n"
          "    if (tid == 0) { const u64 sh_t3 = __builtin_amdgcn_s_memrealtime();\n"
          "        atomicAdd(&g_acc[0], sh_t1 - sh_t0); atomicAdd(&g_acc[1], sh_t2 - sh_t1); atomicAdd(&g_acc[2], sh_t3 - sh_t2);\n"
          "        atomicAdd(&g_acc[3], 1ull); atomicAdd(&g_acc[4], (u64)nU); }\n}"),
@@ -109,8 +122,8 @@ PATCHES = {
          "        g_exp[0] = pt0; g_exp[1] = pt1; g_exp[2] = pt2; g_exp[3] = pt3; g_exp[4] = ntiles;\n    }\n}"),
     ],
     "EXP_NORASTER": [
-        ("        for (u32 c = wave; c < nch; c += NW) {",
-         "        for (u32 c = wave; c < (EXP_NORASTER ? 0u : nch); c += NW) {"),
+        ("        for (u32 c = wave; c < nch; c += NWV) {",
+         "        for (u32 c = wave; c < (EXP_NORASTER ? 0u : nch); c += NWV) {"),
     ],
 }
 PRELUDE = """#include <hip/hip_runtime.h>
@@ -128,6 +141,9 @@ extern "C" int ExpGetAcc(unsigned long long* out) {
 extern "C" int ExpResetAcc() {
     unsigned long long z[8] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_acc), z, 64, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+extern "C" int ExpSetTimes(const unsigned long long* in, int n) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_exp), in, (size_t)n * 8, 0, hipMemcpyHostToDevice) == hipSuccess ? n : -1;
 }
 extern "C" int ExpGetItemTimes(unsigned long long* out, int n) {
     if (n > 4 * 65536) n = 4 * 65536;
