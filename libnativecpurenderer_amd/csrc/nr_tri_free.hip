@@ -842,6 +842,19 @@ __device__ __forceinline__ void frag_key(u64* key, const u32* zin, int p, f64 X,
     else if (zq < zin[p]) atomicMax(&key[p], id1);
 }
 
+// Maximum of a non-negative value over the wave (DPP row shifts and row
+// broadcasts as in wave_scan, then lane 63's value): VALU steps instead of a
+// chain of six cross-lane permutes through LDS.
+__device__ __forceinline__ int wave_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ __forceinline__ f64 readlane_f64(f64 v, int lane) {
     const u64 b = __double_as_longlong(v);
     const u32 lo = __builtin_amdgcn_readlane((u32)b, lane), hi = __builtin_amdgcn_readlane((u32)(b >> 32), lane);
@@ -1024,14 +1037,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
                 if (COUNT) myFrags += (unsigned long long)(lxe - lxs);
                 // pixels: blocks of R rows x C columns (C = the widest span
                 // rounded up to a power of two, R = 64 / C), lane -> (row, column)
-                int wmax = lxe - lxs;
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) wmax = max(wmax, __shfl_xor(wmax, d, 64));
+                const int wmax = wave_max(lxe - lxs);
                 const int lc = wmax <= 8 ? 3 : wmax <= 16 ? 4 : wmax <= 32 ? 5 : 6;
                 const int nrows = br1 - br0, R = 64 >> lc;
-                for (int g = 0; g < nrows; g += R) {
-                    const int rl = g + (lane >> lc);
-                    const int xs = __shfl(lxs, rl & 63, 64), xe = __shfl(lxe, rl & 63, 64);
+                // each lane's span packed (xs | xe << 16); a block's spans are
+                // fetched (one lane permute) while the block before it is
+                // rasterised, so the permute latency is not on the loop's chain
+                const int pk = lxs | (lxe << 16);
+                int rl = lane >> lc;
+                int nx = __shfl(pk, rl & 63, 64);
+                for (int g = 0; g < nrows; g += R, rl += R) {
+                    const int cur = nx;
+                    if (g + R < nrows) nx = __shfl(pk, (rl + R) & 63, 64);
+                    const int xs = cur & 0xFFFF, xe = cur >> 16;
                     const int lx = xs + (lane & ((1 << lc) - 1));
                     if (rl >= nrows || lx >= xe) continue;
                     const int r = br0 + rl;
