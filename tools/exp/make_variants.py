@@ -106,8 +106,8 @@ PATCHES = {
          "    if (!EXP_NOF64ST) { dst[0] = cr; dst[1] = cg; dst[2] = cb;\n    if (ipp == 4) dst[3] = ca; }\n"),
     ],
     "EXP_NOU8ST": [   # shading skips the u8 frame stores
-        ("    if (fp.frameU8) {\n        iu8* d8 = fp.frameU8 + p * ipp;",
-         "    if (fp.frameU8 && !EXP_NOU8ST) {\n        iu8* d8 = fp.frameU8 + p * ipp;"),
+        ("    if (fp.frameU8) {\n        const int r8 = nr_to_u8(cr)",
+         "    if (fp.frameU8 && !EXP_NOU8ST) {\n        const int r8 = nr_to_u8(cr)"),
     ],
     "EXP_PLANT": [   # s_memrealtime stamps at the plan kernel's phase boundaries -> g_exp[0..5]
         ("    if (tid < PLAN_NB) bcnt[tid] = 0;\n    __syncthreads();\n    // pass 1",
