@@ -63,6 +63,7 @@ struct TriScratch {
     u64* vis = nullptr; size_t vis_cap = 0; int visNeutral = -1;
     u32 planSeq = 0;                        // sequence number of the last async plan
     u64 lastPairs = 0;                      // capacity estimate for the next batch
+    u32 lastItems = 0;                      // k_vis work items of the last validated batch (grid estimate)
     u32 lastHeavy = 0;                      // dense tiles of the last batch (k_vis workgroup size)
     u64 lastN = 0;                          // its triangle count (k_vis variant choice)
     u64 capOverride = 0;                    // testing: force this pair capacity
@@ -169,7 +170,7 @@ struct TriangleBuffer {
     // a draw under the same key is sized from them and needs no validation
     bool known = false;
     BinKey knownKey;
-    u32 knownPairs = 0, knownHeavy = 0;
+    u32 knownPairs = 0, knownHeavy = 0, knownItems = 0;
 };
 
 // host helpers shared across translation units

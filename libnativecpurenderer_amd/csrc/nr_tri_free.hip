@@ -1196,12 +1196,13 @@ static BinKey bin_key(const BinParams& bp) {
     return k;
 }
 
-static void record_known(TriangleBuffer* tb, const BinKey& key, u32 pairs, u32 heavy) {
+static void record_known(TriangleBuffer* tb, const BinKey& key, u32 pairs, u32 heavy, u32 items) {
     if (!tb) return;
     tb->known = true;
     tb->knownKey = key;
     tb->knownPairs = pairs;
     tb->knownHeavy = heavy;
+    tb->knownItems = items;
 }
 
 // Items the plan kernel aims for when it picks the slice length
@@ -1240,7 +1241,8 @@ static hipEvent_t sync_event() {
 // queued before on the main stream -- so that it overlaps the previous
 // batch's k_vis (only for immutable inputs: a TriangleBuffer).
 static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
-                         bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0) {
+                         bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0,
+                         u32 knownItems = 0) {
     hipStream_t sa = ctx->stream;
     hipStream_t sb = pipelined ? nr_bin_stream_for(ctx->device) : sa;
     TriScratch& sc = ctx->tri;
@@ -1367,7 +1369,20 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         nr_timing_end_on(ctx, NRK_TRI_SCAN, e0, e1, sb);
 
         if (!exact) {
-            grid = (u32)std::min<u64>(F.fitems_cap, 8192);   // grid-stride over the items
+            // grid-stride over the items.  The grid need not cover them all,
+            // only fill the chip: one workgroup per item of a batch of known
+            // totals, else the last validated batch's items + 25 % (>= 1024,
+            // the chip's k_vis workgroup slots) -- not the capacity bound, whose
+            // surplus workgroups (45 % of a C3 launch, 90 % of an 8-way share's)
+            // were dispatched only to exit (NR_GRID_EST=0: the capacity bound)
+            static const bool gridEst = [] {
+                const char* e = getenv("NR_GRID_EST");
+                return e ? atoi(e) != 0 : true;
+            }();
+            u64 g = F.fitems_cap;
+            if (gridEst && knownItems) g = knownItems;
+            else if (gridEst && sc.lastItems) g = std::max<u64>((u64)sc.lastItems + sc.lastItems / 4, 1024);
+            grid = (u32)std::min<u64>(std::min<u64>(g, F.fitems_cap), 8192);
             break;
         }
         // exact: read the totals back; if the list or the items did not fit,
@@ -1375,6 +1390,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         NR_CHECK(hipStreamSynchronize(sb));
         sc.lastPairs = F.h_plan[0];
         sc.lastHeavy = F.h_plan[5];
+        sc.lastItems = F.h_plan[1];
         sc.lastN = (u64)src.n;
         grid = F.h_plan[1];
         if (F.h_plan[3]) break;
@@ -1454,6 +1470,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         sc.lastN = (u64)src.n;
         sc.lastPairs = tb->knownPairs;
         sc.lastHeavy = tb->knownHeavy;
+        sc.lastItems = tb->knownItems;
     }
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % bin_sets();
@@ -1463,10 +1480,10 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         return e ? atoi(e) != 0 : true;
     }();
     if (!free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact, &seq,
-                      known ? tb->knownPairs : 0))
+                      known ? tb->knownPairs : 0, known ? tb->knownItems : 0))
         return;
     if (exact) {
-        record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy);
+        record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems);
     } else if (!known) {
         PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq, tb, key};
         ctx->pendingBatch = pb;
@@ -1506,7 +1523,8 @@ void settle(RenderContext* ctx) {
     sc.lastN = (u64)pb->src.n;
     sc.lastPairs = F.h_plan[0];
     sc.lastHeavy = F.h_plan[5];
-    record_known(pb->tb, pb->key, F.h_plan[0], F.h_plan[5]);   // exact totals, whether or not they fitted
+    sc.lastItems = F.h_plan[1];
+    record_known(pb->tb, pb->key, F.h_plan[0], F.h_plan[5], F.h_plan[1]);   // exact totals, fitted or not
     if (!F.h_plan[3]) {
         // overflow: the batch's later kernels did nothing; re-run it exactly
         // on the main stream, after everything queued so far
