@@ -69,6 +69,34 @@ __global__ __launch_bounds__(256) void k_tile_ranges(const u32* __restrict__ key
     if (i == P - 1 || keys[i + 1] != k) end[k] = i + 1;
 }
 
+__device__ __forceinline__ u32 wave_min_u32(u32 v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, (u32)__shfl_xor((int)v, d, 64));
+    return v;
+}
+
+// True when every pixel the exact span rule covers quantises (nr_quantize_depth)
+// strictly below zmin, so the LESS test passes on all of them.  For a
+// triangle with G = max|edge| / |den|, bbox extent S and coordinate magnitude
+// M, G*S <= 1e4 and G*M <= 1e4 bound the computed barycentrics of covered
+// pixels to [-1e-10, 1 + 1e-10] (span-rule crossings and the w1/w2
+// expressions both err by O(u (G S + G M)), u = 2^-53; den's cancellation by
+// O(u G S) relative), so with |z| <= 2 the computed depth is at most
+// max(z) + 1e-9 (< max(z) + 1e-8, the bound used).  Anything else: false.
+__device__ __forceinline__ bool zpass_all(const f64 (&sx)[3], const f64 (&sy)[3], f64 e1x, f64 e1y, f64 e2x, f64 e2y,
+                                          f64 den, f64 z0, f64 z1, f64 z2, u32 zmin) {
+    if (!tri_finite(sx, sy) || den == 0) return false;
+    if (!(fabs(z0) <= 2 && fabs(z1) <= 2 && fabs(z2) <= 2)) return false;   // (NaN: false)
+    const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
+    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+    const f64 e = fmax(fmax(fabs(e1x), fabs(e1y)), fmax(fabs(e2x), fabs(e2y)));
+    const f64 G = e / fabs(den);
+    const f64 S = (xmx - xmn) + (ymx - ymn) + 4.0;
+    const f64 M = fmax(fmax(fabs(xmn), fabs(xmx)), fmax(fabs(ymn), fabs(ymx))) + 1.0;
+    if (!(G * S <= 1e4 && G * M <= 1e4)) return false;
+    return nr_quantize_depth(fmax(fmax(z0, z1), z2) + 1e-8) < zmin;
+}
+
 // LDS staging slots of a chunk (SoA, CH entries each)
 enum {
     S_X0 = 0, S_Y0, S_X1, S_Y1, S_X2, S_Y2,   // screen-space vertices
@@ -95,6 +123,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     __shared__ iu8 XS[CH][TH], XE[CH][TH];
     __shared__ iu8 NE[CH][NWAVE];
     __shared__ iu8 VALID[CH];
+    __shared__ iu8 ZPASS[CH];   // depth test known to pass on every covered pixel (see zpass_all)
+    __shared__ u32 zmin_w[NWAVE];
     __shared__ unsigned long long fragSum;
     if (COUNT && tid == 0) fragSum = 0;
 
@@ -122,6 +152,20 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const f64 ct0 = fp.ct[0], ct1 = fp.ct[1], ct2 = fp.ct[2], ct3 = fp.ct[3];
     const f64 wlim = (f64)(fp.W - x0 < TW ? fp.W - x0 : TW);
     unsigned long long myFrags = 0;
+    // Z test without Z write: the tile's depth is constant for the whole
+    // batch, so a triangle whose every covered pixel provably quantises below
+    // the tile's smallest depth passes the test everywhere (zpass_all) and its
+    // fragments skip the depth expression -- the same result, bit for bit.
+    u32 zTileMin = 0;
+    if (DEPTH && !fp.depthWrite) {
+        u32 m = min(min(cz[0], cz[1]), min(cz[2], cz[3]));
+        m = wave_min_u32(m);
+        if (lane == 0) zmin_w[wave] = m;
+        __syncthreads();
+        zTileMin = zmin_w[0];
+#pragma unroll
+        for (int w = 1; w < NWAVE; ++w) zTileMin = min(zTileMin, zmin_w[w]);
+    }
 
     for (u32 base = ls; base < le; base += CH) {
         const int cnt = (le - base) < (u32)CH ? (int)(le - base) : CH;
@@ -142,6 +186,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 f64 z0 = 0, z1 = 0, z2 = 0;
                 if (fp.src.z) { z0 = fp.src.z[t * 3]; z1 = fp.src.z[t * 3 + 1]; z2 = fp.src.z[t * 3 + 2]; }
                 S[S_Z0][tid] = z0; S[S_DZ1][tid] = z1 - z0; S[S_DZ2][tid] = z2 - z0;
+                ZPASS[tid] = !fp.depthWrite && zpass_all(sx, sy, e1x, e1y, e2x, e2y, den, z0, z1, z2, zTileMin);
             }
             if (GOURAUD) {
                 const f64* c = fp.src.rgba + t * 12;
@@ -190,11 +235,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         const f64 X = (f64)(x0 + lane);
         for (int k = 0; k < cnt; ++k) {
             if (!NE[k][wave]) continue;
+            const bool ztest = DEPTH && !ZPASS[k];   // (uniform) the depth expression is needed
             const f64 sx0 = S[S_X0][k], sy0 = S[S_Y0][k];
             const f64 e1x = S[S_E1X][k], e1y = S[S_E1Y][k], e2x = S[S_E2X][k], e2y = S[S_E2Y][k];
             const f64 inv = S[S_INV][k];
             f64 pa = 0, pb = 0;   // dx * e2y, dx * e1y of this lane's column
-            if (DEPTH || GOURAUD) {
+            if (ztest || GOURAUD) {
                 const f64 dx = X - sx0;
                 pa = dx * e2y;
                 pb = dx * e1y;
@@ -212,13 +258,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 const int xs = XS[k][row], xe = XE[k][row];
                 if (lane < xs || lane >= xe) continue;
                 f64 w1 = 0, w2 = 0;
-                if (DEPTH || GOURAUD) {
+                if (ztest || GOURAUD) {
                     const f64 dy = (f64)(y0 + row) - sy0;
                     w1 = (pa - e2x * dy) * inv;
                     w2 = (e1x * dy - pb) * inv;
                 }
                 u32 zq = 0;
-                if (DEPTH) {
+                if (ztest) {
                     const f64 zz = S[S_Z0][k] + S[S_DZ1][k] * w1 + S[S_DZ2][k] * w2;
                     zq = nr_quantize_depth(zz);
                     if (!(zq < cz[r])) continue;
