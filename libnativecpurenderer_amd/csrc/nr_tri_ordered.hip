@@ -105,8 +105,16 @@ enum {
     S_C0,                                      // colour c0[4] (flat: the colour)
     S_D1 = S_C0 + 4,                           // c1-c0 [4] (Gouraud)
     S_D2 = S_D1 + 4,                           // c2-c0 [4] (Gouraud)
-    S_NSLOT = S_D2 + 4
+    // flat: ApplyPixel's per-triangle terms (cpp:529-535), formed once at setup
+    S_FR = S_D2 + 4, S_FG, S_FB, S_FA,         // src * colourTransform
+    S_OM, S_RA, S_GA, S_BA,                    // 1 - a, src * a
+    S_NSLOT
 };
+
+__device__ __forceinline__ u64 uniform_u64(u64 v) {   // (a wave-uniform value into scalar registers)
+    return ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)v);
+}
 
 template <bool GOURAUD, bool DEPTH, bool COUNT>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
@@ -120,8 +128,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
 
     __shared__ f64 S[S_NSLOT][CH];
-    __shared__ iu8 XS[CH][TH], XE[CH][TH];
-    __shared__ iu8 NE[CH][NWAVE];
+    // a wave's 4 row spans of triangle k, packed: byte 2r = xs, 2r + 1 = xe of
+    // row r (an empty row is 0, 0, so 0 = the triangle misses the wave's rows)
+    __shared__ u64 SP[CH][NWAVE];
     __shared__ iu8 VALID[CH];
     __shared__ iu8 ZPASS[CH];   // depth test known to pass on every covered pixel (see zpass_all)
     __shared__ u32 zmin_w[NWAVE];
@@ -200,6 +209,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 const f64* c = fp.src.rgba + t * 4;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) S[S_C0 + k][tid] = c[k];
+                const f64 fR = c[0] * ct0, fG = c[1] * ct1, fB = c[2] * ct2, fA = c[3] * ct3;
+                S[S_FR][tid] = fR; S[S_FG][tid] = fG; S[S_FB][tid] = fB; S[S_FA][tid] = fA;
+                S[S_OM][tid] = 1 - fA;
+                S[S_RA][tid] = fR * fA; S[S_GA][tid] = fG * fA; S[S_BA][tid] = fB * fA;
             }
         }
         __syncthreads();
@@ -207,7 +220,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         {
             const int k = tid >> 3, rg = tid & 7;
             if (k < cnt) {
-                bool any = false;
+                u64 sp = 0;
                 const bool ok = VALID[k];
                 const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
                 const f64 sy[3] = {S[S_Y0][k], S[S_Y1][k], S[S_Y2][k]};
@@ -217,12 +230,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     const i64 gy = y0 + row;
                     int xs = 0, xe = 0;
                     if (ok && gy < fp.H) row_span(sx, sy, (f64)gy, (f64)x0, wlim, xs, xe);
-                    XS[k][row] = (iu8)xs;
-                    XE[k][row] = (iu8)xe;
-                    any = any || xs < xe;
+                    if (xs < xe) sp |= ((u64)xs | ((u64)xe << 8)) << (16 * r);
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
                 }
-                NE[k][rg] = any;
+                SP[k][rg] = sp;
             }
         }
         __syncthreads();
@@ -234,8 +245,37 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         // trees, so the result is bit-identical to the per-pixel form.
         const f64 X = (f64)(x0 + lane);
         for (int k = 0; k < cnt; ++k) {
-            if (!NE[k][wave]) continue;
+            const u64 sp = uniform_u64(SP[k][wave]);
+            if (!sp) continue;
             const bool ztest = DEPTH && !ZPASS[k];   // (uniform) the depth expression is needed
+            if (!GOURAUD && !ztest) {
+                // flat colour, no per-pixel depth: ApplyPixel from the
+                // per-triangle terms on the covered lanes of each row
+                const f64 fA = S[S_FA][k];
+                if (fA != 1) {
+                    const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
+                        if (lane >= xs && lane < xe) {
+                            cr[r] = cr[r] * om + RA;
+                            cg[r] = cg[r] * om + GA;
+                            cb[r] = cb[r] * om + BA;
+                            ca[r] = fA;
+                        }
+                    }
+                } else {
+                    const f64 fR = S[S_FR][k], fG = S[S_FG][k], fB = S[S_FB][k];
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
+                        if (lane >= xs && lane < xe) {
+                            cr[r] = fR; cg[r] = fG; cb[r] = fB; ca[r] = fA;
+                        }
+                    }
+                }
+                continue;
+            }
             const f64 sx0 = S[S_X0][k], sy0 = S[S_Y0][k];
             const f64 e1x = S[S_E1X][k], e1y = S[S_E1Y][k], e2x = S[S_E2X][k], e2y = S[S_E2Y][k];
             const f64 inv = S[S_INV][k];
@@ -246,16 +286,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 pb = dx * e1y;
             }
             f64 fR = 0, fG = 0, fB = 0, fA = 1, om = 0, RA = 0, GA = 0, BA = 0;
-            if (!GOURAUD) {   // ApplyPixel's per-triangle terms (cpp:529-535)
-                fR = S[S_C0 + 0][k] * ct0; fG = S[S_C0 + 1][k] * ct1;
-                fB = S[S_C0 + 2][k] * ct2; fA = S[S_C0 + 3][k] * ct3;
-                om = 1 - fA;
-                RA = fR * fA; GA = fG * fA; BA = fB * fA;
+            if (!GOURAUD) {   // ApplyPixel's per-triangle terms (cpp:529-535), formed at setup
+                fR = S[S_FR][k]; fG = S[S_FG][k]; fB = S[S_FB][k]; fA = S[S_FA][k];
+                om = S[S_OM][k];
+                RA = S[S_RA][k]; GA = S[S_GA][k]; BA = S[S_BA][k];
             }
 #pragma unroll
             for (int r = 0; r < RPW; ++r) {
                 const int row = wave * RPW + r;
-                const int xs = XS[k][row], xe = XE[k][row];
+                const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
                 if (lane < xs || lane >= xe) continue;
                 f64 w1 = 0, w2 = 0;
                 if (ztest || GOURAUD) {

@@ -107,6 +107,42 @@ def test_c5_blend_overdraw_reduced(gpu, oracle):
     assert_same(g, o, "C5/10")
 
 
+def _zpass_edges_frame(fac, W, H):
+    """Z test without write over a non-uniform depth layer, with depths at the
+    edge of the ordered raster's per-triangle pass proof (zpass_all): a
+    written layer at z = 0.5 (+ per-triangle offsets), then blended batches
+    whose depths sit 1e-12 .. 1e-6 below / at / above it, near-1 depths over
+    the cleared 0xFFFFFFFF buffer, slivers and huge coordinates."""
+    g = np.random.default_rng(77)
+    ctx = fac.context(W, H, False)
+    ctx.set_color(0.25, 0.25, 0.25, 0.25)
+    ctx.set_depth_state(True, True)
+    ctx.clear_depth()
+    xy, _, c = scenes.triangle_soup(60, W, H, 60.0, seed=5)
+    z = 0.5 + g.choice([0.0, 1e-9, -1e-9, 3e-7], size=(60, 1)) + np.zeros((60, 3))
+    ctx.draw_triangles(xy, c, z=z)   # opaque layer, Z written
+    ctx.set_depth_state(True, False)
+    for k, off in enumerate([-1e-6, -1e-9, -1e-12, 0.0, 1e-12, 1e-9]):
+        xy, _, c = scenes.triangle_soup(80, W, H, 90.0, seed=100 + k, alpha=(0.2, 0.8))
+        z = np.full((80, 3), 0.5 + off) + g.uniform(0, 1e-10, size=(80, 3)) * (k % 2)
+        ctx.draw_triangles(xy, c, z=z)
+    # over the cleared buffer only: depths at and just below 1
+    ctx.clear_depth()
+    xy, _, c = scenes.triangle_soup(80, W, H, 90.0, seed=300, alpha=(0.2, 0.8))
+    z = 1.0 - g.choice([0.0, 1e-15, 1e-12, 1e-9, 1e-7], size=(80, 3))
+    ctx.draw_triangles(xy, c, z=z)
+    # slivers (ill-conditioned: the proof must decline them) and huge coordinates
+    sl = np.array([[10, 10, 250, 11, 130, 10.5], [5, 120, 6, 5, 5.5, 60], [0, 0, 1e6, 1, -1e6, 2],
+                   [-3e7, 64, 3e7, 65, 0, -3e7]], np.float64)
+    cs = np.tile(np.array([[0.9, 0.1, 0.3, 0.5]]), (len(sl), 1))
+    ctx.draw_triangles(sl, cs, z=np.full((len(sl), 3), 0.999999))
+    return {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer(), "u8": ctx.get_buffer_as_uint8_numpy()}
+
+
+def test_depth_pass_proof_edges(gpu, oracle):
+    assert_same(_zpass_edges_frame(gpu, 256, 160), _zpass_edges_frame(oracle, 256, 160), "zpass edges")
+
+
 @pytest.mark.slow
 def test_c5_blend_overdraw_full(gpu, oracle):
     """C5 at its full size (BASELINE configs[4]: 50k large alpha-blended
