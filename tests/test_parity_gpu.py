@@ -181,6 +181,28 @@ def test_triangle_buffer_equals_host_arrays(gpu):
     assert_same(a, {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, "buffer")
 
 
+def _grid_growth_frame(fac, W, H):
+    """A tiny opaque batch, then one with ~20x its work items, in one context:
+    the second batch's k_vis grid is estimated from the first (last items
+    + 25 %, >= 1024 workgroups), far fewer than its items, so the grid-stride
+    loop must cover the rest; then a smaller batch again (grid > items)."""
+    ctx = fac.context(W, H, False)
+    ctx.set_color(0.5, 0.5, 0.5, 0.5)
+    ctx.set_depth_state(True, True)
+    ctx.clear_depth()
+    for n, spread, seed in [(40, 6.0, 21), (1200000, 2.0, 22), (300, 40.0, 23)]:
+        xy, z, c = scenes.triangle_soup(n, W, H, spread, seed=seed, gouraud=True)
+        ctx.draw_triangles(xy, c, z=z)
+    return {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}
+
+
+def test_kvis_grid_smaller_than_items(gpu, oracle):
+    # 1024x1024: 512 tiles, so the first batch's 512 items give a grid of 1024
+    # workgroups; the 1.2M-triangle batch puts ~2300 pairs in every tile
+    # (3 slices each): ~1500 items for those 1024 workgroups
+    assert_same(_grid_growth_frame(gpu, 1024, 1024), _grid_growth_frame(oracle, 1024, 1024), "grid growth")
+
+
 def test_triangle_buffer_repeat_draws_sized_from_known_totals(gpu):
     """A TriangleBuffer drawn again under the binning key (transform, frame,
     shard) of its last validated draw is sized from the recorded totals and
