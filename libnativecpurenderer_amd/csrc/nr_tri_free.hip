@@ -749,11 +749,59 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
                                            const u64* key, unsigned char* lds, u32& nU) {
     using St = ShadeStage<GOURAUD>;
     constexpr int PPT = TH * TW / NT;
+    const int tid = threadIdx.x;
+#ifndef NR_FLAT_DIRECT
+#define NR_FLAT_DIRECT 1
+#endif
+    if constexpr (!GOURAUD && NR_FLAT_DIRECT) {
+        // Flat: a winner's colour is its rgb -- no record to stage, so no
+        // winner dedup: each pixel loads its winner's colour itself (the few
+        // distinct winners of a tile stay in L2), FQ pixels' loads in flight
+        // at a time.
+        constexpr int FQ = 4;
+        static_assert(PPT % FQ == 0, "pixel groups");
+#pragma unroll 1
+        for (int k0 = 0; k0 < PPT; k0 += FQ) {
+            u32 id[FQ];
+            f64 c[FQ][3];
+#pragma unroll
+            for (int j = 0; j < FQ; ++j) {
+                const int p = tid + (k0 + j) * NT, lx = p & (TW - 1), ly = p / TW;
+                id[j] = 0;
+                if (lx >= wlim || ly >= hlim) continue;
+                const u64 kv = key[ly * (TW + 1) + lx];
+                id[j] = (u32)kv;
+                store_depth<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx, kv);
+                if (id[j]) {
+                    const f64* q = fp.src.rgba + ((i64)id[j] - 1) * 4;
+                    const double2 rg = *reinterpret_cast<const double2*>(q);
+                    c[j][0] = rg.x; c[j][1] = rg.y; c[j][2] = q[2];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < FQ; ++j) {
+                const int p = tid + (k0 + j) * NT, lx = p & (TW - 1), ly = p / TW;
+                if (lx >= wlim || ly >= hlim) continue;
+                const i64 px = x0 + lx, py = y0 + ly;
+                const i64 gp = py * fp.W + px;
+                if (!id[j]) {
+                    if (fp.pendColor) {
+                        const f64 v = fp.pendColorValue;
+                        store_colour(fp, gp, px, py, v, v, v, v);
+                    }
+                    continue;
+                }
+                f64 cr = c[j][0], cg = c[j][1], cb = c[j][2], ca = 1.0;   // (record_colour's flat case)
+                apply_winner(fp, gp, cr, cg, cb, ca);
+                store_colour(fp, gp, px, py, cr, cg, cb, ca);
+            }
+        }
+        return;
+    }
     u32* ht = reinterpret_cast<u32*>(lds + St::HT);
     unsigned short* hidx = reinterpret_cast<unsigned short*>(lds + St::HIDX);
     u32* didx = reinterpret_cast<u32*>(lds + St::DIDX);
     f64* rec = reinterpret_cast<f64*>(lds + St::KEY_OFF);   // over the keys, after pass 1
-    const int tid = threadIdx.x;
     for (int i = tid; i < HTS; i += NT) ht[i] = 0;
     if (tid == 0) nU = 0;
     __syncthreads();
