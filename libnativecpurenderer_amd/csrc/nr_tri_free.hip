@@ -610,6 +610,10 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 #endif
 constexpr int HTS = NR_HTS;    // hash slots (power of two)
 constexpr int MAXPROBE = 16;   // linear-probe limit: a winner not placed / found within it loads directly
+#ifndef NR_OVF_Q
+#define NR_OVF_Q 1
+#endif
+constexpr int OVF_Q = NR_OVF_Q;   // directly loaded records in flight per thread (0: one at a time, in pass 3)
 
 template <bool GOURAUD>
 struct ShadeStage {
@@ -697,28 +701,54 @@ __device__ __forceinline__ void store_clear(const FrameParams& fp, i64 p, i64 px
     store_depth<ZMODE>(fp, p, 0);
 }
 
-// Shading record of triangle t (the expressions of the per-pixel path, once).
+// A winner's source data for its shading record: vertices and the rgb of
+// each vertex (alpha is not needed, see ShadeStage), loaded as 16 + 8 bytes
+// per vertex colour.
 template <bool GOURAUD>
-__device__ __forceinline__ void make_record(const FrameParams& fp, i64 t, f64* r) {
-    if (GOURAUD) {
+struct RecordSrc {
+    f64 p[GOURAUD ? 6 : 1];
+    f64 c[GOURAUD ? 9 : 3];
+};
+
+template <bool GOURAUD>
+__device__ __forceinline__ void load_record_src(const FrameParams& fp, i64 t, RecordSrc<GOURAUD>& s) {
+    if constexpr (GOURAUD) load_tri_xy(fp.src.xy, t, s.p);
+    const int nv = GOURAUD ? 3 : 1, stride = GOURAUD ? 12 : 4;
+#pragma unroll
+    for (int v = 0; v < nv; ++v) {
+        const f64* q = fp.src.rgba + t * stride + 4 * v;
+        const double2 rg = *reinterpret_cast<const double2*>(q);
+        s.c[3 * v] = rg.x; s.c[3 * v + 1] = rg.y; s.c[3 * v + 2] = q[2];
+    }
+}
+
+// Shading record from its source (the expressions of the per-pixel path, once).
+template <bool GOURAUD>
+__device__ __forceinline__ void build_record(const FrameParams& fp, const RecordSrc<GOURAUD>& s, f64* r) {
+    if constexpr (GOURAUD) {
         f64 sx[3], sy[3];
-        tri_screen(fp.src, fp.m, t, sx, sy);
-        f64 c[12];
-        load_tri_rgba<12>(fp.src.rgba, t, c);
+#pragma unroll
+        for (int v = 0; v < 3; ++v) nr_xform(fp.m, s.p[2 * v], s.p[2 * v + 1], sx[v], sy[v]);
         const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
         r[0] = sx[0]; r[1] = sy[0]; r[2] = e1x; r[3] = e1y; r[4] = e2x; r[5] = e2y;
         r[6] = 1.0 / (e1x * e2y - e2x * e1y);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            r[7 + k] = c[k];
-            r[10 + k] = c[4 + k] - c[k];
-            r[13 + k] = c[8 + k] - c[k];
+            r[7 + k] = s.c[k];
+            r[10 + k] = s.c[3 + k] - s.c[k];
+            r[13 + k] = s.c[6 + k] - s.c[k];
         }
     } else {
-        f64 c[4];
-        load_tri_rgba<4>(fp.src.rgba, t, c);
-        r[0] = c[0]; r[1] = c[1]; r[2] = c[2];
+        r[0] = s.c[0]; r[1] = s.c[1]; r[2] = s.c[2];
     }
+}
+
+// Shading record of triangle t.
+template <bool GOURAUD>
+__device__ __forceinline__ void make_record(const FrameParams& fp, i64 t, f64* r) {
+    RecordSrc<GOURAUD> s;
+    load_record_src<GOURAUD>(fp, t, s);
+    build_record<GOURAUD>(fp, s, r);
 }
 
 // Colour of pixel (px, py) from a record.
@@ -749,6 +779,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
                                            const u64* key, unsigned char* lds, u32& nU) {
     using St = ShadeStage<GOURAUD>;
     constexpr int PPT = TH * TW / NT;
+    static_assert(PPT <= 32, "overflow bitmask");
     const int tid = threadIdx.x;
 #ifndef NR_FLAT_DIRECT
 #define NR_FLAT_DIRECT 1
@@ -808,6 +839,11 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
     u32 ids[PPT];
 #pragma unroll
     for (int k = 0; k < PPT; ++k) ids[k] = 0;
+    // bit k: pixel k's winner is not staged -- its record is loaded directly
+    // in pass 3b, OVF_Q pixels at a time.  A dense tile (more distinct
+    // winners than RT, e.g. the many-sliver tiles at a mesh's poles) stops
+    // inserting once RT winners are staged instead of probing a full table.
+    u32 ovf = 0;
 #pragma unroll 1
     for (int k = 0; k < PPT; ++k) {
         const int p = tid + k * NT, lx = p & (TW - 1), ly = p / TW;
@@ -819,21 +855,28 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
             if (q == k) ids[q] = id;   // static register index
         store_depth<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx, kv);
         if (!id) continue;
+        if (OVF_Q && __hip_atomic_load(&nU, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (u32)St::RT) {
+            ovf |= 1u << k;
+            continue;
+        }
         u32 h = ht_hash(id);
+        bool placed = false;
         for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
             const u32 cur = ht[h];
-            if (cur == id) break;
+            if (cur == id) { placed = true; break; }
             if (cur == 0) {
                 const u32 old = atomicCAS(&ht[h], 0u, id);
                 if (old == 0) {
                     const u32 d = atomicAdd(&nU, 1u);
                     hidx[h] = (unsigned short)(d < (u32)St::RT ? d : St::RT);
                     if (d < (u32)St::RT) didx[d] = id;
+                    placed = d < (u32)St::RT;
                     break;
                 }
-                if (old == id) break;
+                if (old == id) { placed = true; break; }
             }
         }
+        if (OVF_Q && !placed) ovf |= 1u << k;
     }
     __syncthreads();   // every key read: the records may overwrite them
     const u32 U = nU < (u32)St::RT ? nU : (u32)St::RT;
@@ -856,6 +899,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
             }
             continue;
         }
+        if ((ovf >> k) & 1u) continue;
         int d = St::RT;
         u32 h = ht_hash(id);
         for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
@@ -866,6 +910,9 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         f64 cr, cg, cb, ca;
         if (d < St::RT) {
             record_colour<GOURAUD>(rec + d * St::REC, px, py, cr, cg, cb, ca);
+        } else if (OVF_Q) {
+            ovf |= 1u << k;
+            continue;
         } else {   // overflow: load this pixel's winner directly
             f64 r[St::REC];
             make_record<GOURAUD>(fp, (i64)id - 1, r);
@@ -873,6 +920,41 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         }
         apply_winner(fp, gp, cr, cg, cb, ca);
         store_colour(fp, gp, px, py, cr, cg, cb, ca);
+    }
+    // pass 3b: pixels whose winner is not staged, OVF_Q at a time: their
+    // records' loads are independent and in flight together
+    if constexpr (OVF_Q > 0) {
+#pragma unroll 1
+        while (ovf) {
+            constexpr int Q = OVF_Q > 0 ? OVF_Q : 1;
+            int kq[Q];
+            RecordSrc<GOURAUD> src[Q];
+#pragma unroll
+            for (int j = 0; j < Q; ++j) {
+                kq[j] = -1;
+                if (!ovf) continue;
+                kq[j] = __builtin_ctz(ovf);
+                ovf &= ovf - 1;
+                u32 id = 0;
+#pragma unroll
+                for (int q = 0; q < PPT; ++q)
+                    if (q == kq[j]) id = ids[q];
+                load_record_src<GOURAUD>(fp, (i64)id - 1, src[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < Q; ++j) {
+                if (kq[j] < 0) continue;
+                const int p = tid + kq[j] * NT, lx = p & (TW - 1), ly = p / TW;
+                const i64 px = x0 + lx, py = y0 + ly;
+                const i64 gp = py * fp.W + px;
+                f64 r[St::REC];
+                build_record<GOURAUD>(fp, src[j], r);
+                f64 cr, cg, cb, ca;
+                record_colour<GOURAUD>(r, px, py, cr, cg, cb, ca);
+                apply_winner(fp, gp, cr, cg, cb, ca);
+                store_colour(fp, gp, px, py, cr, cg, cb, ca);
+            }
+        }
     }
 }
 

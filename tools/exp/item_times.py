@@ -39,8 +39,9 @@ nsl = ((info >> 32) & 0xFFFF).astype(np.int64)
 base = t0.min()
 s, e = (t0 - base) / 100.0, (t1 - base) / 100.0   # us
 dur = e - s
-tm = a[:, 3].astype(np.int64)
-mid = np.where(tm > 0, (tm - base) / 100.0, e)
+tm = (a[:, 3] & 0xFFFFFFFF).astype(np.int64)       # raster barrier, relative to the item start
+tm2 = (a[:, 3] >> 32).astype(np.int64)             # split slices: after the merge
+mid = np.where(tm > 0, s + tm / 100.0, e)
 ras = mid - s          # item start -> raster barrier (key init + raster)
 sha = e - mid          # shading (+ split-tile merge)
 span = e.max()

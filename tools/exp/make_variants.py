@@ -60,14 +60,17 @@ PATCHES = {
          "    for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {\n"
          "        if (tid == 0) { const u64 now = __builtin_amdgcn_s_memrealtime();\n"
          "            if (exp_prev != ~0u) exp_record(exp_prev, exp_t0, now, exp_info, exp_mid);\n"
-         "            exp_prev = item; exp_t0 = now; const uint4 dd = items[item];\n"
+         "            exp_prev = item; exp_t0 = now; exp_mid = 0; const uint4 dd = items[item];\n"
          "            exp_info = (u64)(dd.z - dd.y) | ((u64)dd.w << 32) | ((u64)blockIdx.x << 48); }\n"),
         ("    }   // work items\n",
          "    }   // work items\n"
          "    if (tid == 0 && exp_prev != ~0u) exp_record(exp_prev, exp_t0, __builtin_amdgcn_s_memrealtime(), exp_info, exp_mid);\n"),
         ("        __syncthreads();\n        if (!multi) {   // the whole list was in this slice: shade now\n",
-         "        __syncthreads();\n        if (tid == 0) exp_mid = __builtin_amdgcn_s_memrealtime();\n"
+         "        __syncthreads();\n        if (tid == 0) exp_mid = __builtin_amdgcn_s_memrealtime() - exp_t0;\n"
          "        if (!multi) {   // the whole list was in this slice: shade now\n"),
+        # split slices: clock after the merge + slice counter (high word, relative to the item start)
+        ("        if (!sLast) continue;\n",
+         "        if (tid == 0) exp_mid |= (__builtin_amdgcn_s_memrealtime() - exp_t0) << 32;\n        if (!sLast) continue;\n"),
     ],
     "EXP_SHT": [   # shading phase durations summed over all shade_tile calls -> g_acc
         ("    for (int i = tid; i < HTS; i += NT) ht[i] = 0;\n",
@@ -155,7 +158,8 @@ extern "C" int ExpGetItemTimes(unsigned long long* out, int n) {
 def parse(n):
     if "=" in n:
         n, spec = n.split("=", 1)
-        return n, [f"-D{d}" for d in spec.split("+")], []
+        defs = spec.split("+")
+        return n, [f"-D{d}" for d in defs], [d.split("=")[0] for d in defs if d.split("=")[0] in PATCHES]
     return n, [f"-D{d}=1" for d in VARIANTS[n]], VARIANTS[n]
 
 
