@@ -174,6 +174,8 @@ bool GatherFramebufferEx(RenderContext* ctx, NrComm* comm, i64 root, bool withDe
                                                        every rank (it alone decides the posted send/recvs) */
 bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root); /* tests: GatherFrameU8's packed assembly of n
                                                                     shards of one process, device copies for RCCL */
+bool GatherFrameU8LocalRccl(RenderContext** ctxs, i64 n, i64 root, NrComm* self); /* tests: the same with the packs
+                                              moved by RCCL send/recv pairs over a one-rank communicator `self` */
 
 /* ---- NEW: deferred command list ---------------------------
  * Replaces the reference's recording proxy MultiThreadedVideoRenderContext-

@@ -108,6 +108,7 @@ DEVICE_ABI = {
     "GatherFramebuffer": (B, (P, P, L)),
     "GatherFramebufferEx": (B, (P, P, L, B)),
     "GatherFrameU8Local": (B, (P, L, L)),
+    "GatherFrameU8LocalRccl": (B, (P, L, L, P)),
     "CreateMilthmHitEffectTextures": (B, (P, D, P, L, D, D, D, P)),
     "EnableKernelTiming": (None, (P, B)),
     "GetKernelTiming": (B, (P, ctypes.c_char_p, P, P)),

@@ -530,7 +530,26 @@ bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root) {
 // packing, slot layout, unpack kernel, gather stream and frame-buffer
 // rotation, so the multi-GPU assembly (and its overlap with the next frame)
 // is checked on a single GPU.
-bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
+static bool gather_local(RenderContext** ctxs, i64 n, i64 root, NrComm* self);
+
+bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) { return gather_local(ctxs, n, root, nullptr); }
+
+// NEW (testing): GatherFrameU8Local with the peers' packs moved by RCCL
+// instead of device copies: one ncclGroupStart/End of a send and a receive
+// per peer over a one-rank communicator of this process (`self`, a
+// send/receive pair to its own rank), on the root's gather stream -- the RCCL
+// calls of GatherFrameU8 exercised on one GPU.
+bool GatherFrameU8LocalRccl(RenderContext** ctxs, i64 n, i64 root, NrComm* self) {
+    if (!self || self->nranks != 1) {
+        nr_set_error_msg("GatherFrameU8LocalRccl: need a one-rank communicator");
+        return false;
+    }
+    return gather_local(ctxs, n, root, self);
+}
+
+}  // extern "C"
+
+static bool gather_local(RenderContext** ctxs, i64 n, i64 root, NrComm* self) {
     if (n < 1 || root < 0 || root >= n) {
         nr_set_error_msg("GatherFrameU8Local: need 0 <= root < n");
         return false;
@@ -554,7 +573,7 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     ensure_comm_stream(rc);
     const int xr = rc->frameCur;
     if (!ensure_stage(rc, xr, (size_t)(n * peerStride))) return false;
-    for (i64 p = 0; p < n; ++p) {   // peers: pack on their stream, copy on the root's gather stream
+    for (i64 p = 0; p < n; ++p) {   // peers: pack on their stream, the root's gather stream waits
         if (p == root) continue;
         RenderContext* c = ctxs[p];
         ensure_comm_stream(c);
@@ -564,9 +583,26 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
         band_copy(c, c->frameBuf[xp], c->stageBuf[xp], c->stream, false, (int)p, 0);
         NR_CHECK(hipEventRecord(c->evFrameReady, c->stream));
         NR_CHECK(hipStreamWaitEvent(rc->commStream, c->evFrameReady, 0));
-        NR_CHECK(hipMemcpyAsync(rc->stageBuf[xr] + p * peerStride, c->stageBuf[xp], cnt, hipMemcpyDeviceToDevice,
-                                rc->commStream));
     }
+    Rccl* r = self ? rccl() : nullptr;
+    if (self && !r) return false;
+    bool ok = !self || nccl_ok(r, r->GroupStart(), "ncclGroupStart");
+    for (i64 p = 0; p < n && ok; ++p) {   // the packs into the root's slots
+        if (p == root) continue;
+        RenderContext* c = ctxs[p];
+        const size_t cnt = (size_t)owned_bytes(c, (int)p);
+        if (cnt == 0) continue;
+        iu8* dst = rc->stageBuf[xr] + p * peerStride;
+        const iu8* src = c->stageBuf[c->frameCur];
+        if (!self) {
+            NR_CHECK(hipMemcpyAsync(dst, src, cnt, hipMemcpyDeviceToDevice, rc->commStream));
+            continue;
+        }
+        ok = nccl_ok(r, r->Send(src, cnt, ncclUint8, 0, self->comm, rc->commStream), "ncclSend") &&
+             nccl_ok(r, r->Recv(dst, cnt, ncclUint8, 0, self->comm, rc->commStream), "ncclRecv");
+    }
+    if (self) ok = nccl_ok(r, r->GroupEnd(), "ncclGroupEnd") && ok;
+    if (!ok) return false;
     NR_CHECK(hipEventRecord(rc->evFrameReady, rc->stream));
     NR_CHECK(hipStreamWaitEvent(rc->commStream, rc->evFrameReady, 0));
     band_copy(rc, rc->frameBuf[xr], rc->stageBuf[xr], rc->commStream, true, (int)root, peerStride);
@@ -582,6 +618,8 @@ bool GatherFrameU8Local(RenderContext** ctxs, i64 n, i64 root) {
     rotate_frame(rc, xr);
     return true;
 }
+
+extern "C" {
 
 // NEW: copy the frame of the last GatherFrameU8 to the host (the assembled
 // image on the root; a rank's own bands elsewhere).

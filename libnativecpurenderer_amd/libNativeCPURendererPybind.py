@@ -378,6 +378,14 @@ class RenderContext:
         if not lib.GatherFrameU8Local(arr, len(ctxs), root):
             raise RuntimeError("GatherFrameU8Local failed: " + _lib.last_error())
 
+    @staticmethod
+    def gather_frame_u8_local_rccl(ctxs: typing.Sequence["RenderContext"], self_comm: "Comm", root: int = 0):
+        """Testing: gather_frame_u8_local with the packs moved by RCCL
+        send/recv pairs over a one-rank communicator of this process."""
+        arr = (ctypes.c_void_p * len(ctxs))(*[c._ptr for c in ctxs])
+        if not lib.GatherFrameU8LocalRccl(arr, len(ctxs), root, self_comm._ptr):
+            raise RuntimeError("GatherFrameU8LocalRccl failed: " + _lib.last_error())
+
     def get_frame_yuv420p(self) -> np.ndarray:
         """YUV420P planes (Y, then U, then V) of the last gathered frame,
         converted on the GPU (GetFrameYUV420P; W and H even)."""

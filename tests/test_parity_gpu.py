@@ -393,15 +393,26 @@ def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque):
                                                            (8, 0, 512, 1000, False, [6, 2, 2, 2, 2, 2, 2, 2]),
                                                            (3, 1, 334, 250, False, None)])
 @pytest.mark.parametrize("fmt", ["rgb", "yuv420p"])
-def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha, slots, fmt):
+@pytest.mark.parametrize("via", ["copy", "rccl"])
+def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha, slots, fmt, via):
     """GatherFrameU8's assembly (each rank's bands packed into one message,
-    one unpack on the root), run for n shards on one GPU with device copies in
-    place of RCCL: the root's frame output (u8 image, or its YUV420P planes:
-    a band's Y rows and its U and V rows) equals the unsharded frame byte for
-    byte (odd widths take the byte-wise copy, multiples of 16 the vector one)."""
+    one unpack on the root), run for n shards on one GPU with device copies
+    (via="copy") or RCCL send/recv pairs over a one-rank communicator (via=
+    "rccl": GatherFrameU8's group calls on the hardware) in place of the
+    inter-process transfers: the root's frame output (u8 image, or its YUV420P
+    planes: a band's Y rows and its U and V rows) equals the unsharded frame
+    byte for byte (odd widths take the byte-wise copy, multiples of 16 the
+    vector one)."""
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     if fmt == "yuv420p" and (W % 2 or H % 2):
         pytest.skip("YUV420P needs even sizes")
+    if via == "rccl":
+        comm = R.Comm(1, 0, R.Comm.unique_id())
+
+        def gather(ctxs, root):
+            R.RenderContext.gather_frame_u8_local_rccl(ctxs, comm, root)
+    else:
+        gather = R.RenderContext.gather_frame_u8_local
     xy, z, c = scenes.triangle_soup(2000, W, H, 18, seed=43, gouraud=True)
 
     def render(n, r):
@@ -420,7 +431,7 @@ def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha,
     if fmt == "yuv420p":   # the raster's fused planes = the restatement of its u8 image
         assert np.array_equal(want, scenes.yuv420p(ref.get_buffer_as_uint8_numpy()))
     ctxs = [render(nshards, r) for r in range(nshards)]
-    R.RenderContext.gather_frame_u8_local(ctxs, root)
+    gather(ctxs, root)
     got = ctxs[root].get_frame_u8()
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
     # more frames: the assembly alternates between two frame buffers and
@@ -435,7 +446,7 @@ def test_packed_band_gather_assembles_the_frame(gpu, nshards, root, W, H, alpha,
                 ctx.clear_depth()
                 ctx.draw_triangles(xy[f * 300:], c[f * 300:], z=z[f * 300:])
         ref.gather_frame_u8()
-        R.RenderContext.gather_frame_u8_local(ctxs, root)
+        gather(ctxs, root)
         got = ctxs[root].get_frame_u8()
         want = ref.get_frame_u8()
         assert np.array_equal(got, want), (f, np.argwhere(got != want)[:5])
