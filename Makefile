@@ -4,10 +4,10 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG = libnativecpurenderer_amd
 SRC = $(PKG)/csrc
-OBJ = build/obj
+OBJ ?= build/obj
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Wno-unused-function \
-           -fno-gpu-rdc -Wno-pass-failed -I$(SRC)
-LIB = $(PKG)/libNativeCPURenderer.so
+           -fno-gpu-rdc -Wno-pass-failed -I$(SRC) $(EXTRA)
+LIB ?= $(PKG)/libNativeCPURenderer.so
 SRCS = $(wildcard $(SRC)/*.hip)
 OBJS = $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(SRCS))
 

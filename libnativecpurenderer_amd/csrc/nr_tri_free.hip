@@ -789,7 +789,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         // winner dedup: each pixel loads its winner's colour itself (the few
         // distinct winners of a tile stay in L2), FQ pixels' loads in flight
         // at a time.
-        constexpr int FQ = 4;
+        constexpr int FQ = PPT < 4 ? PPT : 4;
         static_assert(PPT % FQ == 0, "pixel groups");
 #pragma unroll 1
         for (int k0 = 0; k0 < PPT; k0 += FQ) {
