@@ -26,6 +26,9 @@ constexpr int RPW = 4;           // rows per wave
 constexpr int NWAVE = TH / RPW;  // 8
 constexpr int WG = NWAVE * 64;   // 512 threads
 constexpr int CH = 64;           // triangles staged per chunk
+#ifndef NR_C5_IB
+#define NR_C5_IB 1   // blend-only loop: lane mask from the span by inverse ballot (1) or lane compares (0)
+#endif
 
 __global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt) {
     const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
@@ -116,7 +119,18 @@ __device__ __forceinline__ u64 uniform_u64(u64 v) {   // (a wave-uniform value i
            (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)v);
 }
 
-template <bool GOURAUD, bool DEPTH, bool COUNT>
+// Lanes [xs, xe) of a row's span word (xs | xe << 8) as a wave mask: built with
+// scalar instructions and used as the lane condition directly (inverse ballot),
+// no per-lane compares.
+__device__ __forceinline__ u64 span_lanes(u32 w16) {
+    const u32 xs = w16 & 0xFFu, xe = w16 >> 8;
+    const u64 hi = xe >= 64 ? ~0ull : ((1ull << xe) - 1), lo = (1ull << xs) - 1;
+    return hi & ~lo;
+}
+
+// RGBA: the context has an alpha channel (ipp 4).  An RGB context never
+// stores alpha, so the per-fragment alpha moves are dropped.
+template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
                                                     const u32* __restrict__ tstart, const u32* __restrict__ tend) {
     const int tile = blockIdx.x;
@@ -139,7 +153,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
     // ---- the tile's pixel state, resident in registers for the whole list
     const i64 px = x0 + lane;
-    const int ipp = fp.ipp;
+    constexpr int ipp = RGBA ? 4 : 3;
     f64 cr[RPW], cg[RPW], cb[RPW], ca[RPW];
     u32 cz[RPW];
 #pragma unroll
@@ -153,13 +167,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             } else {
                 const f64* p = fp.fb + (py * fp.W + px) * ipp;
                 cr[r] = p[0]; cg[r] = p[1]; cb[r] = p[2];
-                if (ipp == 4) ca[r] = p[3];
+                if (RGBA) ca[r] = p[3];
             }
             if (DEPTH) cz[r] = fp.pendDepth ? fp.pendDepthValue : fp.depth[py * fp.W + px];
         }
     }
     const f64 ct0 = fp.ct[0], ct1 = fp.ct[1], ct2 = fp.ct[2], ct3 = fp.ct[3];
     const f64 wlim = (f64)(fp.W - x0 < TW ? fp.W - x0 : TW);
+    const u32 fullw = (u32)wlim << 8;   // span word of a row covered from column 0 to wlim
     unsigned long long myFrags = 0;
     // Z test without Z write: the tile's depth is constant for the whole
     // batch, so a triangle whose every covered pixel provably quantises below
@@ -215,7 +230,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 S[S_RA][tid] = fR * fA; S[S_GA][tid] = fG * fA; S[S_BA][tid] = fB * fA;
             }
         }
-        __syncthreads();
+        // a chunk of flat translucent triangles whose depth test is proven to
+        // pass (or off) takes the blend-only loop below (C5's common case)
+        bool blendOnly = !GOURAUD;
+        if (!GOURAUD && tid < cnt) {
+            const bool zok = !DEPTH || ZPASS[tid] || !VALID[tid];
+            blendOnly = zok && S[S_FA][tid] != 1;
+        }
+        const bool allBlend = __syncthreads_and(blendOnly ? 1 : 0) != 0;
         // ---- (b) exact coverage spans: thread = (triangle k, wave-row group rg)
         {
             const int k = tid >> 3, rg = tid & 7;
@@ -243,25 +265,66 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         // over the triangle (flat: src * colourTransform, src * a, 1 - a) is
         // formed once there: the same rounded values in the same expression
         // trees, so the result is bit-identical to the per-pixel form.
+        if (!GOURAUD && allBlend) {
+            // every triangle of the chunk: ApplyPixel from the per-triangle
+            // terms on the covered lanes (a loop with one path, so the pixel
+            // registers are updated in place)
+            for (int k = 0; k < cnt; ++k) {
+                const u64 sp = uniform_u64(SP[k][wave]);
+                if (!sp) continue;
+                const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
+                const f64 fA = RGBA ? S[S_FA][k] : 0.0;
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    const u32 w16 = (u32)(sp >> (16 * r)) & 0xFFFFu;
+#if NR_C5_IB
+                    if (__builtin_amdgcn_inverse_ballot_w64(span_lanes(w16))) {
+#else
+                    const int xs = (int)(w16 & 0xFF), xe = (int)(w16 >> 8);
+                    if (lane >= xs && lane < xe) {
+#endif
+                        cr[r] = cr[r] * om + RA;
+                        cg[r] = cg[r] * om + GA;
+                        cb[r] = cb[r] * om + BA;
+                        if (RGBA) ca[r] = fA;
+                    }
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         const f64 X = (f64)(x0 + lane);
         for (int k = 0; k < cnt; ++k) {
             const u64 sp = uniform_u64(SP[k][wave]);
             if (!sp) continue;
-            const bool ztest = DEPTH && !ZPASS[k];   // (uniform) the depth expression is needed
+            // (uniform: read into scalar registers, so the branches below are scalar)
+            const bool ztest = DEPTH && !__builtin_amdgcn_readfirstlane((int)ZPASS[k]);   // the depth expression is needed
             if (!GOURAUD && !ztest) {
                 // flat colour, no per-pixel depth: ApplyPixel from the
                 // per-triangle terms on the covered lanes of each row
-                const f64 fA = S[S_FA][k];
+                const f64 fA = __longlong_as_double((long long)uniform_u64((u64)__double_as_longlong(S[S_FA][k])));
+                // A row the span covers from column 0 to the tile's last
+                // on-screen column (the span word 0 | wl << 8: a scalar test)
+                // is blended on every lane: lanes past wl hold off-screen
+                // pixels that are never stored.  Other rows test the lane.
                 if (fA != 1) {
                     const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
+                        const u32 w16 = (u32)(sp >> (16 * r)) & 0xFFFFu;
+                        if (w16 == fullw) {
+                            cr[r] = cr[r] * om + RA;
+                            cg[r] = cg[r] * om + GA;
+                            cb[r] = cb[r] * om + BA;
+                            if (RGBA) ca[r] = fA;
+                            continue;
+                        }
+                        const int xs = (int)(w16 & 0xFF), xe = (int)(w16 >> 8);
                         if (lane >= xs && lane < xe) {
                             cr[r] = cr[r] * om + RA;
                             cg[r] = cg[r] * om + GA;
                             cb[r] = cb[r] * om + BA;
-                            ca[r] = fA;
+                            if (RGBA) ca[r] = fA;
                         }
                     }
                 } else {
@@ -270,7 +333,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     for (int r = 0; r < RPW; ++r) {
                         const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
                         if (lane >= xs && lane < xe) {
-                            cr[r] = fR; cg[r] = fG; cb[r] = fB; ca[r] = fA;
+                            cr[r] = fR; cg[r] = fG; cb[r] = fB;
+                            if (RGBA) ca[r] = fA;
                         }
                     }
                 }
@@ -294,8 +358,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
             for (int r = 0; r < RPW; ++r) {
                 const int row = wave * RPW + r;
+#if NR_C5_IB
+                if (!__builtin_amdgcn_inverse_ballot_w64(span_lanes((u32)(sp >> (16 * r)) & 0xFFFFu))) continue;
+#else
                 const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
                 if (lane < xs || lane >= xe) continue;
+#endif
                 f64 w1 = 0, w2 = 0;
                 if (ztest || GOURAUD) {
                     const f64 dy = (f64)(y0 + row) - sy0;
@@ -320,14 +388,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         G = cg[r] * (1 - A) + G * A;
                         B = cb[r] * (1 - A) + B * A;
                     }
-                    cr[r] = R; cg[r] = G; cb[r] = B; ca[r] = A;
+                    cr[r] = R; cg[r] = G; cb[r] = B;
+                    if (RGBA) ca[r] = A;
                 } else if (fA != 1) {
                     cr[r] = cr[r] * om + RA;
                     cg[r] = cg[r] * om + GA;
                     cb[r] = cb[r] * om + BA;
-                    ca[r] = fA;
+                    if (RGBA) ca[r] = fA;
                 } else {
-                    cr[r] = fR; cg[r] = fG; cb[r] = fB; ca[r] = fA;
+                    cr[r] = fR; cg[r] = fG; cb[r] = fB;
+                    if (RGBA) ca[r] = fA;
                 }
                 if (DEPTH && fp.depthWrite) cz[r] = zq;
             }
@@ -342,7 +412,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (px < fp.W && py < fp.H) {
             f64* p = fp.fb + (py * fp.W + px) * ipp;
             p[0] = cr[r]; p[1] = cg[r]; p[2] = cb[r];
-            if (ipp == 4) p[3] = ca[r];
+            if (RGBA) p[3] = ca[r];
             if (DEPTH && (fp.depthWrite || fp.pendDepth)) fp.depth[py * fp.W + px] = cz[r];
         }
     }
@@ -355,7 +425,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
 template <bool G, bool D, bool C>
 void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s) {
-    hipLaunchKernelGGL((k_tile_raster<G, D, C>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te);
+    if (fp.ipp == 4) hipLaunchKernelGGL((k_tile_raster<G, D, C, true>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te);
+    else hipLaunchKernelGGL((k_tile_raster<G, D, C, false>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te);
 }
 
 template <bool C>
