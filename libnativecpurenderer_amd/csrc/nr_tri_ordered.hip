@@ -145,6 +145,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // a wave's 4 row spans of triangle k, packed: byte 2r = xs, 2r + 1 = xe of
     // row r (an empty row is 0, 0, so 0 = the triangle misses the wave's rows)
     __shared__ u64 SP[CH][NWAVE];
+    // span-phase ballots: HITW[w] byte g = which of triangles 8w..8w+7 touch
+    // the rows of wave g (bit j: triangle 8w + j)
+    __shared__ u64 HITW[NWAVE];
     __shared__ iu8 VALID[CH];
     __shared__ iu8 ZPASS[CH];   // depth test known to pass on every covered pixel (see zpass_all)
     __shared__ u32 zmin_w[NWAVE];
@@ -238,11 +241,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             blendOnly = zok && S[S_FA][tid] != 1;
         }
         const bool allBlend = __syncthreads_and(blendOnly ? 1 : 0) != 0;
-        // ---- (b) exact coverage spans: thread = (triangle k, wave-row group rg)
+        // ---- (b) exact coverage spans: thread = (triangle k, wave-row group rg);
+        // wave w takes triangles 8w..8w+7, lane = rg * 8 + (k - 8w), so the
+        // wave's ballot of "touches the rows" holds one byte per row group
         {
-            const int k = tid >> 3, rg = tid & 7;
+            const int k = (wave << 3) | (lane & 7), rg = lane >> 3;
+            u64 sp = 0;
             if (k < cnt) {
-                u64 sp = 0;
                 const bool ok = VALID[k];
                 const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
                 const f64 sy[3] = {S[S_Y0][k], S[S_Y1][k], S[S_Y2][k]};
@@ -257,8 +262,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 }
                 SP[k][rg] = sp;
             }
+            const u64 hit = __ballot(sp != 0);
+            if (lane == 0) HITW[wave] = hit;
         }
         __syncthreads();
+        // this wave's triangles of the chunk (bit k: triangle k touches its rows)
+        u64 hm = 0;
+#pragma unroll
+        for (int w = 0; w < NWAVE; ++w) hm |= ((uniform_u64(HITW[w]) >> (8 * wave)) & 0xFFull) << (8 * w);
         // ---- (c) in-order raster of the chunk; each wave owns 4 rows.
         // Every product of the per-pixel expressions that is constant along
         // a column (dx * e2y, dx * e1y), along a row (e2x * dy, e1x * dy) or
@@ -269,11 +280,26 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             // every triangle of the chunk: ApplyPixel from the per-triangle
             // terms on the covered lanes (a loop with one path, so the pixel
             // registers are updated in place)
-            for (int k = 0; k < cnt; ++k) {
-                const u64 sp = uniform_u64(SP[k][wave]);
-                if (!sp) continue;
-                const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
-                const f64 fA = RGBA ? S[S_FA][k] : 0.0;
+            // only the triangles touching this wave's rows; the next one's
+            // span and terms are read while the current one blends
+            int k = hm ? (int)__builtin_ctzll(hm) : 0;
+            u64 spn = 0;
+            f64 omn = 0, RAn = 0, GAn = 0, BAn = 0, fAn = 0;
+            if (hm) {
+                spn = SP[k][wave];
+                omn = S[S_OM][k]; RAn = S[S_RA][k]; GAn = S[S_GA][k]; BAn = S[S_BA][k];
+                if (RGBA) fAn = S[S_FA][k];
+            }
+            while (hm) {
+                hm &= hm - 1;
+                const u64 sp = uniform_u64(spn);
+                const f64 om = omn, RA = RAn, GA = GAn, BA = BAn, fA = fAn;
+                if (hm) {
+                    k = (int)__builtin_ctzll(hm);
+                    spn = SP[k][wave];
+                    omn = S[S_OM][k]; RAn = S[S_RA][k]; GAn = S[S_GA][k]; BAn = S[S_BA][k];
+                    if (RGBA) fAn = S[S_FA][k];
+                }
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
                     const u32 w16 = (u32)(sp >> (16 * r)) & 0xFFFFu;
@@ -294,9 +320,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             continue;
         }
         const f64 X = (f64)(x0 + lane);
-        for (int k = 0; k < cnt; ++k) {
+        for (; hm; hm &= hm - 1) {
+            const int k = (int)__builtin_ctzll(hm);
             const u64 sp = uniform_u64(SP[k][wave]);
-            if (!sp) continue;
             // (uniform: read into scalar registers, so the branches below are scalar)
             const bool ztest = DEPTH && !__builtin_amdgcn_readfirstlane((int)ZPASS[k]);   // the depth expression is needed
             if (!GOURAUD && !ztest) {
