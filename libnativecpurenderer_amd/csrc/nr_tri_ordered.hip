@@ -26,9 +26,6 @@ constexpr int RPW = 4;           // rows per wave
 constexpr int NWAVE = TH / RPW;  // 8
 constexpr int WG = NWAVE * 64;   // 512 threads
 constexpr int CH = 64;           // triangles staged per chunk
-#ifndef NR_C5_IB
-#define NR_C5_IB 1   // blend-only loop: lane mask from the span by inverse ballot (1) or lane compares (0)
-#endif
 
 __global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt) {
     const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
@@ -119,13 +116,20 @@ __device__ __forceinline__ u64 uniform_u64(u64 v) {   // (a wave-uniform value i
            (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)v);
 }
 
-// Lanes [xs, xe) of a row's span word (xs | xe << 8) as a wave mask: built with
-// scalar instructions and used as the lane condition directly (inverse ballot),
-// no per-lane compares.
+// A row's coverage span [xs, xe) within the tile as a 16-bit word:
+// xs | (64 - xe) << 8, an empty row as 63 | 1 << 8.  Its lanes as a wave mask
+// take two shifts and an AND of scalar registers (the empty row's shifts leave
+// no bit), and the mask is the lane condition itself (inverse ballot): no
+// per-lane compares.
+constexpr u32 SPAN_EMPTY = 63u | (1u << 8);
+__device__ __forceinline__ u32 span_word(int xs, int xe) {
+    return xs < xe ? (u32)xs | ((u32)(64 - xe) << 8) : SPAN_EMPTY;
+}
 __device__ __forceinline__ u64 span_lanes(u32 w16) {
-    const u32 xs = w16 & 0xFFu, xe = w16 >> 8;
-    const u64 hi = xe >= 64 ? ~0ull : ((1ull << xe) - 1), lo = (1ull << xs) - 1;
-    return hi & ~lo;
+    return (~0ull << (w16 & 63u)) & (~0ull >> ((w16 >> 8) & 63u));
+}
+__device__ __forceinline__ bool span_lane(u64 sp, int r) {   // this lane in row r's span (sp: the wave's 4 rows)
+    return __builtin_amdgcn_inverse_ballot_w64(span_lanes((u32)(sp >> (16 * r)) & 0xFFFFu));
 }
 
 // RGBA: the context has an alpha channel (ipp 4).  An RGB context never
@@ -136,14 +140,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int tile = blockIdx.x;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
     const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // (wave: uniform, so the per-wave masks and addresses below stay scalar)
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     if (!owned_row(ty, fp.period, fp.mask)) return;
     const u32 ls = tstart[tile], le = tend[tile];
     if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
 
     __shared__ f64 S[S_NSLOT][CH];
-    // a wave's 4 row spans of triangle k, packed: byte 2r = xs, 2r + 1 = xe of
-    // row r (an empty row is 0, 0, so 0 = the triangle misses the wave's rows)
+    // a wave's 4 row spans of triangle k: bits 16r..16r+15 = span_word of row r
     __shared__ u64 SP[CH][NWAVE];
     // span-phase ballots: HITW[w] byte g = which of triangles 8w..8w+7 touch
     // the rows of wave g (bit j: triangle 8w + j)
@@ -177,7 +181,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     const f64 ct0 = fp.ct[0], ct1 = fp.ct[1], ct2 = fp.ct[2], ct3 = fp.ct[3];
     const f64 wlim = (f64)(fp.W - x0 < TW ? fp.W - x0 : TW);
-    const u32 fullw = (u32)wlim << 8;   // span word of a row covered from column 0 to wlim
     unsigned long long myFrags = 0;
     // Z test without Z write: the tile's depth is constant for the whole
     // batch, so a triangle whose every covered pixel provably quantises below
@@ -247,6 +250,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         {
             const int k = (wave << 3) | (lane & 7), rg = lane >> 3;
             u64 sp = 0;
+            bool touch = false;
             if (k < cnt) {
                 const bool ok = VALID[k];
                 const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
@@ -257,12 +261,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     const i64 gy = y0 + row;
                     int xs = 0, xe = 0;
                     if (ok && gy < fp.H) row_span(sx, sy, (f64)gy, (f64)x0, wlim, xs, xe);
-                    if (xs < xe) sp |= ((u64)xs | ((u64)xe << 8)) << (16 * r);
+                    sp |= (u64)span_word(xs, xe) << (16 * r);
+                    touch |= xs < xe;
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
                 }
                 SP[k][rg] = sp;
             }
-            const u64 hit = __ballot(sp != 0);
+            const u64 hit = __ballot(touch);
             if (lane == 0) HITW[wave] = hit;
         }
         __syncthreads();
@@ -280,35 +285,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             // every triangle of the chunk: ApplyPixel from the per-triangle
             // terms on the covered lanes (a loop with one path, so the pixel
             // registers are updated in place)
-            // only the triangles touching this wave's rows; the next one's
-            // span and terms are read while the current one blends
-            int k = hm ? (int)__builtin_ctzll(hm) : 0;
-            u64 spn = 0;
-            f64 omn = 0, RAn = 0, GAn = 0, BAn = 0, fAn = 0;
-            if (hm) {
-                spn = SP[k][wave];
-                omn = S[S_OM][k]; RAn = S[S_RA][k]; GAn = S[S_GA][k]; BAn = S[S_BA][k];
-                if (RGBA) fAn = S[S_FA][k];
-            }
-            while (hm) {
-                hm &= hm - 1;
-                const u64 sp = uniform_u64(spn);
-                const f64 om = omn, RA = RAn, GA = GAn, BA = BAn, fA = fAn;
-                if (hm) {
-                    k = (int)__builtin_ctzll(hm);
-                    spn = SP[k][wave];
-                    omn = S[S_OM][k]; RAn = S[S_RA][k]; GAn = S[S_GA][k]; BAn = S[S_BA][k];
-                    if (RGBA) fAn = S[S_FA][k];
-                }
+            // (only the triangles touching this wave's rows)
+            for (; hm; hm &= hm - 1) {
+                const int k = (int)__builtin_ctzll(hm);
+                const u64 spv = SP[k][wave];
+                const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
+                const f64 fA = RGBA ? S[S_FA][k] : 0.0;
+                const u64 sp = uniform_u64(spv);
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
-                    const u32 w16 = (u32)(sp >> (16 * r)) & 0xFFFFu;
-#if NR_C5_IB
-                    if (__builtin_amdgcn_inverse_ballot_w64(span_lanes(w16))) {
-#else
-                    const int xs = (int)(w16 & 0xFF), xe = (int)(w16 >> 8);
-                    if (lane >= xs && lane < xe) {
-#endif
+                    if (span_lane(sp, r)) {
                         cr[r] = cr[r] * om + RA;
                         cg[r] = cg[r] * om + GA;
                         cb[r] = cb[r] * om + BA;
@@ -329,24 +315,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 // flat colour, no per-pixel depth: ApplyPixel from the
                 // per-triangle terms on the covered lanes of each row
                 const f64 fA = __longlong_as_double((long long)uniform_u64((u64)__double_as_longlong(S[S_FA][k])));
-                // A row the span covers from column 0 to the tile's last
-                // on-screen column (the span word 0 | wl << 8: a scalar test)
-                // is blended on every lane: lanes past wl hold off-screen
-                // pixels that are never stored.  Other rows test the lane.
                 if (fA != 1) {
                     const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        const u32 w16 = (u32)(sp >> (16 * r)) & 0xFFFFu;
-                        if (w16 == fullw) {
-                            cr[r] = cr[r] * om + RA;
-                            cg[r] = cg[r] * om + GA;
-                            cb[r] = cb[r] * om + BA;
-                            if (RGBA) ca[r] = fA;
-                            continue;
-                        }
-                        const int xs = (int)(w16 & 0xFF), xe = (int)(w16 >> 8);
-                        if (lane >= xs && lane < xe) {
+                        if (span_lane(sp, r)) {
                             cr[r] = cr[r] * om + RA;
                             cg[r] = cg[r] * om + GA;
                             cb[r] = cb[r] * om + BA;
@@ -357,8 +330,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     const f64 fR = S[S_FR][k], fG = S[S_FG][k], fB = S[S_FB][k];
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
-                        if (lane >= xs && lane < xe) {
+                        if (span_lane(sp, r)) {
                             cr[r] = fR; cg[r] = fG; cb[r] = fB;
                             if (RGBA) ca[r] = fA;
                         }
@@ -384,12 +356,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
             for (int r = 0; r < RPW; ++r) {
                 const int row = wave * RPW + r;
-#if NR_C5_IB
-                if (!__builtin_amdgcn_inverse_ballot_w64(span_lanes((u32)(sp >> (16 * r)) & 0xFFFFu))) continue;
-#else
-                const int xs = (int)(sp >> (16 * r)) & 0xFF, xe = (int)(sp >> (16 * r + 8)) & 0xFF;
-                if (lane < xs || lane >= xe) continue;
-#endif
+                if (!span_lane(sp, r)) continue;
                 f64 w1 = 0, w2 = 0;
                 if (ztest || GOURAUD) {
                     const f64 dy = (f64)(y0 + row) - sy0;
