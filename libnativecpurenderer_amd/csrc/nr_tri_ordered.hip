@@ -108,6 +108,7 @@ enum {
     // flat: ApplyPixel's per-triangle terms (cpp:529-535), formed once at setup
     S_FR = S_D2 + 4, S_FG, S_FB, S_FA,         // src * colourTransform
     S_OM, S_RA, S_GA, S_BA,                    // 1 - a, src * a
+    S_SL0, S_SL1, S_SL2,                       // edge slopes (edge_slopes) for the division-free spans
     S_NSLOT
 };
 
@@ -212,6 +213,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             S[S_X2][tid] = sx[2]; S[S_Y2][tid] = sy[2];
             S[S_E1X][tid] = e1x; S[S_E1Y][tid] = e1y; S[S_E2X][tid] = e2x; S[S_E2Y][tid] = e2y;
             S[S_INV][tid] = 1.0 / den;
+            {
+                f64 sl[3];
+                edge_slopes(sx, sy, sl);
+                S[S_SL0][tid] = sl[0]; S[S_SL1][tid] = sl[1]; S[S_SL2][tid] = sl[2];
+            }
             if (DEPTH) {
                 f64 z0 = 0, z1 = 0, z2 = 0;
                 if (fp.src.z) { z0 = fp.src.z[t * 3]; z1 = fp.src.z[t * 3 + 1]; z2 = fp.src.z[t * 3 + 2]; }
@@ -255,12 +261,18 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 const bool ok = VALID[k];
                 const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
                 const f64 sy[3] = {S[S_Y0][k], S[S_Y1][k], S[S_Y2][k]};
+                const f64 sl[3] = {S[S_SL0][k], S[S_SL1][k], S[S_SL2][k]};
+                // rows with a straddling edge: ymin <= y < ymax, where exactly
+                // two edges straddle (row_span_slopes = row_span there); none
+                // elsewhere (row_span's empty span)
+                const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
                     const int row = rg * RPW + r;
                     const i64 gy = y0 + row;
                     int xs = 0, xe = 0;
-                    if (ok && gy < fp.H) row_span(sx, sy, (f64)gy, (f64)x0, wlim, xs, xe);
+                    if (ok && gy < fp.H && ymn <= (f64)gy && (f64)gy < ymx)
+                        row_span_slopes(sx, sy, sl, (f64)gy, (f64)x0, wlim, xs, xe);
                     sp |= (u64)span_word(xs, xe) << (16 * r);
                     touch |= xs < xe;
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);

@@ -107,6 +107,33 @@ def test_c5_blend_overdraw_reduced(gpu, oracle):
     assert_same(g, o, "C5/10")
 
 
+def _blend_chunks_frame(fac, W, H, alpha, test):
+    """The ordered raster's blend-only chunk loop and its neighbours: flat
+    translucent triangles in 64-triangle chunks where some chunks hold an
+    opaque (a = 1) triangle (those chunks take the general loop), a right-edge
+    tile narrower than 64 columns, spans ending at the tile edge, a colour
+    transform, and Z test on (write off) or off."""
+    ctx = fac.context(W, H, alpha)
+    ctx.set_color(0.3, 0.6, 0.1, 0.7)
+    ctx.set_depth_state(test, False)
+    ctx.clear_depth()
+    ctx.set_color_transform(0.9, 1.0, 0.8, 0.95)
+    xy, z, c = scenes.triangle_soup(1500, W, H, 120.0, seed=4242, alpha=(0.2, 0.8))
+    c = c.copy()
+    c[::97, 3] = 1.0                      # a few opaque triangles: their chunks take the general loop
+    xy[::53, 0::2] = np.clip(xy[::53, 0::2], W - 30, W + 30)   # triangles over the narrow right-edge tile
+    ctx.draw_triangles(xy, c, z=z)
+    return {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer(), "u8": ctx.get_buffer_as_uint8_numpy()}
+
+
+@pytest.mark.parametrize("alpha", [False, True])
+@pytest.mark.parametrize("test", [False, True])
+def test_blend_only_chunks_match_oracle(gpu, oracle, alpha, test):
+    W, H = 360, 200   # 6 tile columns, the last 40 wide; 7 tile rows, the last 8 high
+    assert_same(_blend_chunks_frame(gpu, W, H, alpha, test), _blend_chunks_frame(oracle, W, H, alpha, test),
+                f"blend chunks alpha={alpha} test={test}")
+
+
 def _zpass_edges_frame(fac, W, H):
     """Z test without write over a non-uniform depth layer, with depths at the
     edge of the ordered raster's per-triangle pass proof (zpass_all): a
