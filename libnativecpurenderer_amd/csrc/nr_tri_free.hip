@@ -1001,6 +1001,9 @@ static_assert(TH <= 64, "coop raster: one lane per tile row");
 constexpr f64 COOP_PAIRS = 2.0;
 
 constexpr int NW = VWG / 64;   // waves per k_vis workgroup
+#ifndef NR_HEAVY_PRIO
+#define NR_HEAVY_PRIO 512   // work items of at least this many triangles run at raised wave priority (0: off)
+#endif
 constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 
 // One workgroup per work item (tile, slice of <= SLICE triangles).  The 4
@@ -1047,6 +1050,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
         const int tile = (int)d.x;
         const u32 ls = d.y, le = d.z;
         const bool multi = d.w > 1;
+#if NR_HEAVY_PRIO
+        // the longest work items (dense tiles' slices) set the kernel's
+        // critical path: their waves win the SIMD's issue arbitration over the
+        // short items that run beside them
+        if (le - ls >= (u32)NR_HEAVY_PRIO) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
         const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
