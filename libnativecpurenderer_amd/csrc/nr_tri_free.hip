@@ -1001,6 +1001,9 @@ static_assert(TH <= 64, "coop raster: one lane per tile row");
 constexpr f64 COOP_PAIRS = 2.0;
 
 constexpr int NW = VWG / 64;   // waves per k_vis workgroup
+#ifndef NR_VIS_BASE_PRIO
+#define NR_VIS_BASE_PRIO 0   // wave priority of the other k_vis items (the binning kernels run at 0)
+#endif
 #ifndef NR_HEAVY_PRIO
 #define NR_HEAVY_PRIO 512   // work items of at least this many triangles run at raised wave priority (0: off)
 #endif
@@ -1055,7 +1058,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
         // critical path: their waves win the SIMD's issue arbitration over the
         // short items that run beside them
         if (le - ls >= (u32)NR_HEAVY_PRIO) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(0);
+        else __builtin_amdgcn_s_setprio(NR_VIS_BASE_PRIO);
 #endif
         const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
