@@ -126,9 +126,28 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
 // It also re-zeroes the tile counters for the next batch (after reading them)
 // and the emit cursors, and mirrors the totals into pinned host memory, so a
 // batch needs no memset and no copy command.
+#ifndef NR_ROW_SPLIT
+#define NR_ROW_SPLIT 0   // tiles of at least this many triangles get one item per half tile (rows) per slice; 0: off
+#endif
+__device__ __forceinline__ bool row_split(u32 c) { return NR_ROW_SPLIT > 0 && c >= (u32)NR_ROW_SPLIT; }
 __device__ __forceinline__ u32 tile_items(u32 c, bool owned, u32 slice) {
     // slice is a power of two: the division is a shift
-    return owned ? (c > slice ? (c + slice - 1) >> (31 - __clz(slice)) : 1u) : 0u;
+    const u32 ns = c > slice ? (c + slice - 1) >> (31 - __clz(slice)) : 1u;
+    return owned ? (row_split(c) ? 2 * ns : ns) : 0u;
+}
+// Work item k of the ni items of a tile with c pairs from list offset ea:
+// {tile, slice begin, slice end, w}, w = slices (items sharing the tile's
+// merge, low 16 bits) | row half << 16 (0: whole tile, 1: rows [0, TH/2),
+// 2: rows [TH/2, TH)).  A dense tile (row_split) has two items per slice,
+// one per half: a half-tile item rasterises only its rows, so the dense
+// tiles' items -- the critical path of k_vis -- are half as long.
+__device__ __forceinline__ uint4 tile_item(u32 tile, u32 ea, u32 c, u32 k, u32 ni, u32 slice) {
+    if (!row_split(c)) {
+        const u32 ls = ea + k * slice;
+        return make_uint4(tile, ls, min(ls + slice, ea + c), ni);
+    }
+    const u32 ls = ea + (k >> 1) * slice;
+    return make_uint4(tile, ls, min(ls + slice, ea + c), (ni == 2 ? 1u : ni) | ((1u + (k & 1u)) << 16));
 }
 
 // Inclusive wave scan (64 lanes) with DPP row shifts and row broadcasts
@@ -237,10 +256,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
             off[i] = ea;
             if (fits && ni) {
                 const u32 eb = atomicAdd(&bcur[size_class(c, slice)], ni);
-                for (u32 k = 0; k < ni; ++k) {
-                    const u32 ls = ea + k * slice;
-                    items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + c), ni);
-                }
+                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c, k, ni, slice);
             }
             cnt[i] = 0;
             cur[i] = 0;
@@ -352,10 +368,7 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
             const u32 ni = tile_items(c[j], owned_row(i / tiles_x, period, mask), slice);
             if (fits && ni) {
                 const u32 eb = atomicAdd(&bcur[size_class(c[j], slice)], ni);
-                for (u32 k = 0; k < ni; ++k) {
-                    const u32 ls = ea + k * slice;
-                    items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + c[j]), ni);
-                }
+                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c[j], k, ni, slice);
             }
             cnt[i] = 0;
             cur[i] = 0;
@@ -485,10 +498,7 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
             for (int k = 0; k < PLAN_NB; ++k)
                 if (cls == k) { eb = hc[k]; hc[k] += ni; }
             if (fits)
-                for (u32 k = 0; k < ni; ++k) {
-                    const u32 ls = ea + k * slice;
-                    items[eb + k] = make_uint4((u32)i, ls, min(ls + slice, ea + cj), ni);
-                }
+                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, cj, k, ni, slice);
             ea += cj;
             if (++tx == tiles_x) { tx = 0; ++ty; }
         }
@@ -1052,7 +1062,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
         __syncthreads();
         const int tile = (int)d.x;
         const u32 ls = d.y, le = d.z;
-        const bool multi = d.w > 1;
+        const u32 nsl = d.w & 0xFFFFu, half = d.w >> 16;
+        const bool multi = nsl > 1;
+        const int rlo = half == 2 ? TH / 2 : 0, rhi = half == 1 ? TH / 2 : TH;   // this item's rows
 #if NR_HEAVY_PRIO
         // the longest work items (dense tiles' slices) set the kernel's
         // critical path: their waves win the SIMD's issue arbitration over the
@@ -1064,6 +1076,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
         const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
+        const int rcap = hlim < rhi ? hlim : rhi;   // rows [rlo, rcap) of the tile are rasterised here
         if (ls == le) {   // no triangle: only the pending clears
             for (int p = tid; p < TH * TW; p += NT) {
                 const int lx = p & (TW - 1), ly = p / TW;
@@ -1122,8 +1135,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
             bool big = false;
             if (lane < cnt && tri_finite(sx, sy) && den != 0) {
                 const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
-                r0 = (int)clampd(ceil(ymn) - (f64)y0, 0.0, (f64)hlim);
-                r1 = (int)clampd(ceil(ymx) - (f64)y0, 0.0, (f64)hlim);
+                r0 = (int)clampd(ceil(ymn) - (f64)y0, (f64)rlo, (f64)rcap);
+                r1 = (int)clampd(ceil(ymx) - (f64)y0, (f64)rlo, (f64)rcap);
                 const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
                 const f64 bw = fmin(xmx, (f64)x0 + wlim) - fmax(xmn, (f64)x0);   // bbox width in the tile
                 big = COOP && (f64)(r1 - r0) * bw >= (f64)BIG_PX;
@@ -1207,8 +1220,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
             }
         }
         __syncthreads();
-        if (!multi) {   // the whole list was in this slice: shade now
-            shade_tile<ZMODE, GOURAUD, NT>(fp, x0, y0, wlim, hlim, key, lds, nU);
+        if (!multi) {   // the whole list was in this slice: shade now (this item's rows)
+            if (rlo < rcap)
+                shade_tile<ZMODE, GOURAUD, NT>(fp, x0, y0 + rlo, wlim, rcap - rlo, key + rlo * KS, lds, nU);
             continue;
         }
         // split tile: merge into the global keys; the last slice to finish
@@ -1233,7 +1247,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES
         __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: this wave's atomics performed
         __syncthreads();
         if (tid == 0) {
-            const u32 nsl = d.w;
             const u32 prev = __hip_atomic_fetch_add(&done[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sLast = prev + 1 == nsl;
             if (prev + 1 == nsl) __hip_atomic_store(&done[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1461,8 +1474,9 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         cap = (size_t)std::min<u64>(sc.capOverride ? sc.capOverride : est, 0xFFFFFFF0ull);
         if (!grow_list(cap)) return false;
         if (!sc.capOverride) cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
-        // work items: at most one per tile + one per full slice of the list
-        if (!grow_items((size_t)ntiles + cap / SLICE_MIN + 2)) return false;
+        // work items: at most one per tile + one per full slice of the list,
+        // twice that with dense tiles split into row halves (NR_ROW_SPLIT)
+        if (!grow_items((NR_ROW_SPLIT > 0 ? 2 : 1) * ((size_t)ntiles + cap / SLICE_MIN + 2))) return false;
     } else {
         if (!grow_list(1) || !grow_items(1)) return false;
         cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
