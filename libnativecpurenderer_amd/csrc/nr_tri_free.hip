@@ -1031,8 +1031,10 @@ constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 // pair density -- the variant without it keeps fewer registers live for sliver meshes.
 // NT: workgroup size (VWG, or 2 * VWG for batches with few pairs, whose dense
 // items are latency-bound: more waves per item).
-template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NR_VIS_WAVES_PER_EU))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
+// WPE: waves per SIMD the registers are allocated for (NR_VIS_WAVES_PER_EU, or 3 for large batches: see
+// launch_vis).
+template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT, int WPE = NR_VIS_WAVES_PER_EU>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ vis, u32* __restrict__ done,
                                              const u32* __restrict__ plan) {
@@ -1288,9 +1290,24 @@ static u32 wide_heavy() {
     return v;
 }
 
+// Registers of k_vis for 3 waves per SIMD (up to 168 VGPRs, no spills) on large
+// batches: with one workgroup slot per CU left free by the raster, the next
+// batch's binning kernels run beside it instead of waiting for its tail, and
+// the frame shortens while k_vis itself takes the same time (C3 0.1667 ->
+// 0.1609 ms per frame; profiles/r02_c3/ab_wpe3.txt).  Short batches (C2, an
+// 8-way share) keep 4 waves: their rasters are short and occupancy-bound
+// (+15 % at 3).  NR_VIS_WPE3=0 keeps 4 waves everywhere (A/B).
+static bool vis_wpe3(bool big) {
+    static const int v = [] {
+        const char* e = getenv("NR_VIS_WPE3");
+        return e ? atoi(e) : -1;
+    }();
+    return v >= 0 ? v != 0 : big;
+}
+
 template <int Z, bool C, bool G>
 void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid, hipStream_t s,
-                hipEvent_t stop) {
+                hipEvent_t stop, bool big) {
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
     const bool coop = sc.coopMode ? sc.coopMode == 1
@@ -1305,6 +1322,13 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::F
         else
             hipExtLaunchKernelGGL((k_vis<Z, false, G, false, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, nullptr, stop, 0, fp, F.fitems,
                                F.flist, sc.vis, sc.fdone, F.dplan);
+    } else if (!C && vis_wpe3(big)) {
+        if (coop)
+            hipExtLaunchKernelGGL((k_vis<Z, false, G, true, VWG, 3>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp,
+                                  F.fitems, F.flist, sc.vis, sc.fdone, F.dplan);
+        else
+            hipExtLaunchKernelGGL((k_vis<Z, false, G, false, VWG, 3>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp,
+                                  F.fitems, F.flist, sc.vis, sc.fdone, F.dplan);
     } else if (coop) {
         hipExtLaunchKernelGGL((k_vis<Z, C, G, true, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.vis,
                            sc.fdone, F.dplan);
@@ -1316,9 +1340,9 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::F
 
 template <int Z, bool G>
 void launch_vis_z(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid,
-                  hipStream_t s, hipEvent_t stop) {
-    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, F, grid, s, stop);
-    else launch_vis<Z, false, G>(fp, sc, F, grid, s, stop);
+                  hipStream_t s, hipEvent_t stop, bool big) {
+    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, F, grid, s, stop, big);
+    else launch_vis<Z, false, G>(fp, sc, F, grid, s, stop, big);
 }
 
 // Events of a batch carried by the kernels' own completion signals
@@ -1575,9 +1599,10 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = ext_stop() && !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
-        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa, st); else launch_vis_z<1, false>(fp, sc, F, grid, sa, st); }
-        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa, st); else launch_vis_z<2, false>(fp, sc, F, grid, sa, st); }
-        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa, st); else launch_vis_z<0, false>(fp, sc, F, grid, sa, st); }
+        const bool big = plan_small(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
+        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa, st, big); else launch_vis_z<1, false>(fp, sc, F, grid, sa, st, big); }
+        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa, st, big); else launch_vis_z<2, false>(fp, sc, F, grid, sa, st, big); }
+        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa, st, big); else launch_vis_z<0, false>(fp, sc, F, grid, sa, st, big); }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
