@@ -1422,7 +1422,7 @@ static hipEvent_t sync_event() {
 // batch's k_vis (only for immutable inputs: a TriangleBuffer).
 static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
                          bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0,
-                         u32 knownItems = 0) {
+                         u32 knownItems = 0, bool idle = false) {
     hipStream_t sa = ctx->stream;
     hipStream_t sb = pipelined ? nr_bin_stream_for(ctx->device) : sa;
     TriScratch& sc = ctx->tri;
@@ -1521,7 +1521,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        const bool small = plan_small(fp.period, fp.mask, src.n);
+        const bool small = !idle && plan_small(fp.period, fp.mask, src.n);   // idle GPU: the faster wide plan
         const u32 icap32 = (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull);
         // the register plan: 256 threads whenever the tiles fit (one wave per
         // SIMD, 86 VGPRs: it fits beside running k_vis workgroups, where the
@@ -1661,8 +1661,23 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         const char* e = getenv("NR_BIN_PIPE");
         return e ? atoi(e) != 0 : true;
     }();
-    if (!free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact, &seq,
-                      known ? tb->knownPairs : 0, known ? tb->knownItems : 0))
+    // A batch issued to an idle main stream (the first frame after a readback
+    // or a Flush) has no raster to overlap its binning with: it bins in line
+    // on the main stream, with the wide plan kernel, and k_vis follows without
+    // a cross-queue wait (whose wake-up took ~15 us in the kernel trace,
+    // profiles/r02h_c3).  NR_BIN_IDLE_INLINE=0: always the binning stream (A/B).
+    static const bool idleInline = [] {
+        const char* e = getenv("NR_BIN_IDLE_INLINE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    bool idle = false;
+    if (idleInline && pipeOn && tb != nullptr && !exact) {
+        const hipError_t q = hipStreamQuery(ctx->stream);
+        idle = q == hipSuccess;
+        if (q != hipSuccess) (void)hipGetLastError();   // hipErrorNotReady is an answer, not a failure
+    }
+    if (!free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact && !idle, &seq,
+                      known ? tb->knownPairs : 0, known ? tb->knownItems : 0, idle))
         return;
     if (exact) {
         record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems);
