@@ -619,13 +619,16 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 #define NR_REC_EXTRA 19200
 #endif
 constexpr int HTS = NR_HTS;    // hash slots (power of two)
+#ifndef NR_HTS3
+#define NR_HTS3 1024   // hash slots of the 3-wave instance (its LDS may grow to a third of the CU's)
+#endif
 constexpr int MAXPROBE = 16;   // linear-probe limit: a winner not placed / found within it loads directly
 #ifndef NR_OVF_Q
 #define NR_OVF_Q 1
 #endif
 constexpr int OVF_Q = NR_OVF_Q;   // directly loaded records in flight per thread (0: one at a time, in pass 3)
 
-template <bool GOURAUD>
+template <bool GOURAUD, int HS = HTS>
 struct ShadeStage {
     // Gouraud record: sx0 sy0 e1x e1y e2x e2y inv | c0 rgb | (c1-c0) rgb | (c2-c0) rgb
     // flat record: rgb.  Alpha is not staged: every batch routed here has
@@ -640,12 +643,13 @@ struct ShadeStage {
     static constexpr int EXTRA = GOURAUD ? NR_REC_EXTRA : 0;
     static constexpr int RT_RAW = (KEY_BYTES + EXTRA) / (REC * 8);
     static constexpr int RT = RT_RAW < TH * TW ? RT_RAW : TH * TW;   // staged records per tile
-    static constexpr int HT = 0, HIDX = HTS * 4, DIDX = HTS * 6;
+    static constexpr int HT = 0, HIDX = HS * 4, DIDX = HS * 6;
     static constexpr int KEY_OFF = ((DIDX + RT * 4) + 15) & ~15;
     static constexpr int BYTES = KEY_OFF + KEY_BYTES + EXTRA;
 };
 
-__device__ __forceinline__ u32 ht_hash(u32 id) { return (id * 2654435761u) >> (32 - __builtin_ctz(HTS)); }
+template <int HS>
+__device__ __forceinline__ u32 ht_hash(u32 id) { return (id * 2654435761u) >> (32 - __builtin_ctz(HS)); }
 
 // Depth of a shaded pixel (winner kv; (u32)kv == 0: no fragment won it):
 // the winner's depth, or a pending depth clear.
@@ -784,10 +788,10 @@ __device__ __forceinline__ void record_colour(const f64* r, i64 px, i64 py, f64&
 // global loads: one latency round), written over the keys.  Pass 3: colour,
 // ApplyPixel, framebuffer (+ u8 frame) written once.  A winner past the RT
 // staged records (or not placed within MAXPROBE probes) loads its own record.
-template <int ZMODE, bool GOURAUD, int NT>
+template <int ZMODE, bool GOURAUD, int NT, int HS>
 __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0, int wlim, int hlim,
                                            const u64* key, unsigned char* lds, u32& nU) {
-    using St = ShadeStage<GOURAUD>;
+    using St = ShadeStage<GOURAUD, HS>;
     constexpr int PPT = TH * TW / NT;
     static_assert(PPT <= 32, "overflow bitmask");
     const int tid = threadIdx.x;
@@ -843,7 +847,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
     unsigned short* hidx = reinterpret_cast<unsigned short*>(lds + St::HIDX);
     u32* didx = reinterpret_cast<u32*>(lds + St::DIDX);
     f64* rec = reinterpret_cast<f64*>(lds + St::KEY_OFF);   // over the keys, after pass 1
-    for (int i = tid; i < HTS; i += NT) ht[i] = 0;
+    for (int i = tid; i < HS; i += NT) ht[i] = 0;
     if (tid == 0) nU = 0;
     __syncthreads();
     u32 ids[PPT];
@@ -869,9 +873,9 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
             ovf |= 1u << k;
             continue;
         }
-        u32 h = ht_hash(id);
+        u32 h = ht_hash<HS>(id);
         bool placed = false;
-        for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
+        for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HS - 1)) {
             const u32 cur = ht[h];
             if (cur == id) { placed = true; break; }
             if (cur == 0) {
@@ -911,8 +915,8 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         }
         if ((ovf >> k) & 1u) continue;
         int d = St::RT;
-        u32 h = ht_hash(id);
-        for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HTS - 1)) {
+        u32 h = ht_hash<HS>(id);
+        for (int probe = 0; probe < MAXPROBE; ++probe, h = (h + 1) & (HS - 1)) {
             const u32 cur = ht[h];
             if (cur == id) { d = hidx[h]; break; }
             if (cur == 0) break;
@@ -1044,8 +1048,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // rows at the same column then hit different LDS banks
     // one LDS block (ShadeStage): hash tables | tile keys | extra; the
     // shading records overwrite the keys
-    __shared__ __attribute__((aligned(16))) unsigned char lds[ShadeStage<GOURAUD>::BYTES];
-    u64* const key = reinterpret_cast<u64*>(lds + ShadeStage<GOURAUD>::KEY_OFF);
+    constexpr int HS = WPE == 3 ? NR_HTS3 : HTS;   // the 3-wave instance has LDS to spare for a larger hash table
+    __shared__ __attribute__((aligned(16))) unsigned char lds[ShadeStage<GOURAUD, HS>::BYTES];
+    u64* const key = reinterpret_cast<u64*>(lds + ShadeStage<GOURAUD, HS>::KEY_OFF);
     __shared__ u32 zin[ZMODE == 2 ? TH * KS : 1];
     __shared__ u32 nU;
     __shared__ int sLast;
@@ -1224,7 +1229,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         __syncthreads();
         if (!multi) {   // the whole list was in this slice: shade now (this item's rows)
             if (rlo < rcap)
-                shade_tile<ZMODE, GOURAUD, NT>(fp, x0, y0 + rlo, wlim, rcap - rlo, key + rlo * KS, lds, nU);
+                shade_tile<ZMODE, GOURAUD, NT, HS>(fp, x0, y0 + rlo, wlim, rcap - rlo, key + rlo * KS, lds, nU);
             continue;
         }
         // split tile: merge into the global keys; the last slice to finish
@@ -1265,7 +1270,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             if (gv != neutral) __hip_atomic_store(g, neutral, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        shade_tile<ZMODE, GOURAUD, NT>(fp, x0, y0, wlim, hlim, key, lds, nU);
+        shade_tile<ZMODE, GOURAUD, NT, HS>(fp, x0, y0, wlim, hlim, key, lds, nU);
     }   // work items
     if (COUNT) {
         __syncthreads();
