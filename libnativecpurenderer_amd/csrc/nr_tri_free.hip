@@ -622,7 +622,10 @@ constexpr int HTS = NR_HTS;    // hash slots (power of two)
 #ifndef NR_HTS3
 #define NR_HTS3 1024   // hash slots of the 3-wave instance (its LDS may grow to a third of the CU's)
 #endif
-constexpr int MAXPROBE = 16;   // linear-probe limit: a winner not placed / found within it loads directly
+#ifndef NR_MAXPROBE
+#define NR_MAXPROBE 16
+#endif
+constexpr int MAXPROBE = NR_MAXPROBE;   // linear-probe limit: a winner not placed / found within it loads directly
 #ifndef NR_OVF_Q
 #define NR_OVF_Q 1
 #endif
