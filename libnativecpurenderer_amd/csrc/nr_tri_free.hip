@@ -619,6 +619,9 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 #define NR_REC_EXTRA 19200
 #endif
 constexpr int HTS = NR_HTS;    // hash slots (power of two)
+#ifndef NR_HTS_WIDE
+#define NR_HTS_WIDE 1024   // hash slots of the 512-thread instance (its LDS holds two workgroups per CU)
+#endif
 #ifndef NR_HTS3
 #define NR_HTS3 1024   // hash slots of the 3-wave instance (its LDS may grow to a third of the CU's)
 #endif
@@ -1051,7 +1054,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // rows at the same column then hit different LDS banks
     // one LDS block (ShadeStage): hash tables | tile keys | extra; the
     // shading records overwrite the keys
-    constexpr int HS = WPE == 3 ? NR_HTS3 : HTS;   // the 3-wave instance has LDS to spare for a larger hash table
+    // the 3-wave instance has LDS to spare for a larger hash table, and so has
+    // the 512-thread one (two workgroups per CU)
+    constexpr int HS = WPE == 3 ? NR_HTS3 : NT > VWG ? NR_HTS_WIDE : HTS;
     __shared__ __attribute__((aligned(16))) unsigned char lds[ShadeStage<GOURAUD, HS>::BYTES];
     u64* const key = reinterpret_cast<u64*>(lds + ShadeStage<GOURAUD, HS>::KEY_OFF);
     __shared__ u32 zin[ZMODE == 2 ? TH * KS : 1];
