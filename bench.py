@@ -20,6 +20,11 @@ the timed region (--root-slots auto: candidate weighted patterns timed, the
 fastest kept and reported).  At N=1 the same step runs with a local conversion.
 value = frame fragments (summed over ranks) x steps / max-over-ranks time.
 
+At N=1 the line also carries `extra`: the metric's literal configuration
+(1M triangles at 1920x1080), C2, C5 (with a VALU roofline beside the HBM one)
+and host-delivered frame rates (--deliver host: every step ends with the
+frame on the host, as the video caller needs it), each measured the same way.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -27,6 +32,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -37,15 +43,24 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 PEAK_HBM_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+# f64 VALU: 256 CUs x 4 SIMDs x 16 f64 lanes per clock x 2.4 GHz (78.6 TFLOP/s FP64 vector spec = this x 2 for FMA);
+# a non-FMA f64 add or multiply counts one op
+PEAK_F64_VALU_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 
 CONFIGS = {
     # name: (W, H, kind, params)
     "c3": dict(W=3840, H=2160, mesh=(500, 1000), gouraud=True, desc="C3: 1M-tri displaced UV sphere, 3840x2160, Gouraud, Z LESS+write"),
-    "c3_1080p": dict(W=1920, H=1080, mesh=(500, 1000), gouraud=True, desc="1M-tri displaced UV sphere, 1920x1080, Gouraud, Z LESS+write"),
+    "c3_1080p": dict(W=1920, H=1080, mesh=(500, 1000), gouraud=True, desc="1M-tri displaced UV sphere, 1920x1080, Gouraud, Z LESS+write (the metric's literal configuration)"),
     "c2": dict(W=1920, H=1080, soup=(10000, 32.0, None), gouraud=False, desc="C2: 10k random opaque tris, 1920x1080, flat, Z LESS+write"),
     "c5": dict(W=1920, H=1080, soup=(50000, 256.0, (0.2, 0.8)), gouraud=False, write=False,
                desc="C5: 50k alpha-blended tris back-to-front, 1920x1080, Z test on, write off"),
 }
+
+# f64 VALU operations a blended RGB fragment needs at least: per channel
+# dst*(1-a) + (src*a), with (1-a) and src*a formed once per flat triangle --
+# one multiply and one add (ApplyPixel, cpp:529-547); the depth test of C5 is
+# provably passed per triangle, so it adds none
+BLEND_OPS_PER_FRAGMENT = 6
 
 
 def make_scene(cfg):
@@ -91,33 +106,267 @@ def kernel_bytes(cfg, n_tri, path, frac=1.0, frame_out="rgb"):
     return {"tile_raster": algorithmic_bytes(cfg, n_tri, frac, u8=(path == "order-free"), frame_out=frame_out)}
 
 
+def frame_roofline(B_frame, share, ms, world):
+    """Frame-level HBM fraction.  A real N-GPU line moves the whole job's bytes
+    with N GPUs' bandwidth; an emulated rank share (world 1, share < 1) moves
+    its owned share of the bytes with one GPU's."""
+    nbytes = B_frame if world > 1 else B_frame * share
+    peak = PEAK_HBM_GBPS * max(1, world)
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    return {"frame_algorithmic_bytes": int(nbytes), "frame_achieved": round(achieved, 1),
+            "frame_peak": peak, "frame_frac": round(achieved / peak, 4)}
+
+
+def shard_tag(nsh, slots):
+    if nsh <= 1:
+        return ""
+    return f"_shard0of{nsh}" + ("" if slots is None else "_slots" + "-".join(map(str, slots)))
+
+
+def load_pmc_traffic(cfg_name, nsh=1, slots=None, frame_out="rgb"):
+    """HBM bytes per launch of the dominant kernel from a PMC summary of the SAME
+    configuration and rank share (profiles/pmc_<config><shard tag>.json, written
+    from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes); None when there is none."""
+    tag = cfg_name + shard_tag(nsh, slots) + ("" if frame_out == "rgb" else "_" + frame_out)
+    p = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        if d.get("config") == tag:
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+    return None, None
+
+
+def host_cpu():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
 def cpu_baseline(cfg, xy, z, c, budget_s=10.0, max_frames=50):
-    """The oracle (CPU restatement, single thread) on the same frames."""
+    """The oracle (CPU restatement, single thread) on the same frames, pinned
+    to one core (sched_setaffinity, the equivalent of `taskset -c <cpu>`)."""
     import scenes
     f = scenes.OracleFactory()
     times, frags = [], 0
     ctx = f.context(cfg["W"], cfg["H"], False)
-    t_start = time.perf_counter()
-    while len(times) < max_frames and (time.perf_counter() - t_start < budget_s or len(times) < 2):
-        t0 = time.perf_counter()
-        ctx.set_color(0, 0, 0, 0)
-        ctx.set_depth_state(True, cfg.get("write", True))
-        ctx.clear_depth()
-        ctx.draw_triangles(xy, c, z=z)
-        times.append(time.perf_counter() - t0)
-        frags = ctx.last_fragment_count()
+    old = os.sched_getaffinity(0)
+    cpu = min(old)
+    os.sched_setaffinity(0, {cpu})
+    try:
+        t_start = time.perf_counter()
+        while len(times) < max_frames and (time.perf_counter() - t_start < budget_s or len(times) < 2):
+            t0 = time.perf_counter()
+            ctx.set_color(0, 0, 0, 0)
+            ctx.set_depth_state(True, cfg.get("write", True))
+            ctx.clear_depth()
+            ctx.draw_triangles(xy, c, z=z)
+            times.append(time.perf_counter() - t0)
+            frags = ctx.last_fragment_count()
+    finally:
+        os.sched_setaffinity(0, old)
     med = float(np.median(times))
     return {"value": frags / med / 1e6, "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "pinned_cpu": cpu, "host_cpu": host_cpu(), "host_nproc": os.cpu_count(),
+            "host_affinity_cpus": len(old),
             "sample": f"{len(times)} full frames of the same workload, median {med*1e3:.1f} ms/frame "
-                      f"(oracle/oracle.c, gcc -O3 -ffp-contract=off, 1 thread)"}
+                      f"(oracle/oracle.c, gcc -O3 -ffp-contract=off, 1 thread pinned to cpu {cpu} "
+                      f"= taskset -c {cpu})"}
 
 
-def load_pmc_traffic(cfg_name):
-    p = os.path.join(ROOT, "profiles", f"pmc_{cfg_name}.json")
-    if os.path.exists(p):
-        d = json.load(open(p))
-        return d.get("hbm_bytes_per_launch"), d
-    return None, None
+class Runner:
+    """One configuration in one context: fragment count, breakdown pass, timed
+    region (K frames, barrier + synchronize on both sides, max over ranks)."""
+
+    def __init__(self, R, args, cfg_name, world, rank, dist, rdev, nsh, me, deliver="none"):
+        self.R, self.args, self.cfg_name = R, args, cfg_name
+        self.cfg = CONFIGS[cfg_name]
+        self.world, self.rank, self.dist, self.rdev = world, rank, dist, rdev
+        self.nsh, self.me, self.deliver = nsh, me, deliver
+        cfg = self.cfg
+        self.W, self.H = cfg["W"], cfg["H"]
+        self.xy, self.z, self.c = make_scene(cfg)
+        self.n_tri = len(self.xy)
+        self.ctx = R.RenderContext(self.W, self.H, False)
+        self.ctx.set_frame_format(args.frame_output)
+        if args.force_ordered:
+            self.ctx.set_force_ordered_raster(True)
+        self.buf = R.TriangleBuffer(self.xy, self.c, z=self.z, gouraud=cfg["gouraud"])
+        self.comm = None
+        self.host = None
+        self.tickets = []
+        if deliver == "host":
+            nbytes = int(np.prod(self.ctx.frame_output_shape()))
+            self.host = [R.HostBuffer(nbytes) for _ in range(2)]
+        self.fixed_k = None if args.root_slots in ("auto", "equal") else int(args.root_slots)
+        self.root_k = self.fixed_k
+        self.apply_partition(self.fixed_k)
+
+    def slots_for(self, k):
+        return None if k is None else [k] + [2] * (self.nsh - 1)
+
+    def apply_partition(self, k):
+        if self.nsh <= 1:
+            return
+        if k is None:
+            self.ctx.set_shard(self.nsh, self.me)
+        else:
+            self.ctx.set_shard_slots(self.nsh, self.me, self.slots_for(k))
+
+    def frame(self, i=0):
+        ctx = self.ctx
+        ctx.set_color(0, 0, 0, 0)
+        ctx.set_depth_state(True, self.cfg.get("write", True))
+        ctx.clear_depth()
+        ctx.draw_triangle_buffer(self.buf)
+        ctx.gather_frame_u8(self.comm, 0)
+        if self.host is not None and self.rank == 0:
+            # frame i's D2H runs on the gather stream while frame i+1 renders;
+            # host buffer i % 2 is rewritten only after frame i-2 has landed
+            if len(self.tickets) >= 2:
+                ctx.wait_frame_delivered(self.tickets.pop(0))
+            self.tickets.append(ctx.deliver_frame(self.host[i % 2]))
+
+    def drain(self):
+        self.ctx.flush()
+        while self.tickets:
+            self.ctx.wait_frame_delivered(self.tickets.pop(0))
+
+    def sync(self):
+        import torch
+        torch.cuda.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max_over_ranks(self, v):
+        if self.dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], device=self.rdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def run(self, steps, warmup, calibrate=False):
+        import torch
+        ctx, dist = self.ctx, self.dist
+        # fragment count of one frame (outside the timed region), summed over ranks
+        ctx.set_fragment_counting(True)
+        self.frame()
+        self.drain()
+        frags = ctx.get_fragment_count()
+        ctx.set_fragment_counting(False)
+        if dist is not None:
+            t = torch.tensor([frags], dtype=torch.int64, device=self.rdev)
+            dist.all_reduce(t)
+            frags = int(t.item())
+
+        # partition calibration (N>1, --root-slots auto): every candidate share
+        # of rank 0 is timed over a few frames (max over ranks), the fastest kept
+        calib = {}
+        if calibrate:
+            for k in (None, 3, 4, 5, 6, 8, 10, 12):
+                self.apply_partition(k)
+                for _ in range(3):
+                    self.frame()
+                self.drain()
+                self.sync()
+                t0 = time.perf_counter()
+                for i in range(10):
+                    self.frame(i)
+                self.drain()
+                torch.cuda.synchronize()
+                calib["equal" if k is None else str(k)] = round(self.max_over_ranks(time.perf_counter() - t0) / 10 * 1e3, 4)
+            best = min(calib, key=calib.get)
+            self.root_k = None if best == "equal" else int(best)
+            self.apply_partition(self.root_k)
+
+        for i in range(warmup):
+            self.frame(i)
+        self.drain()
+
+        names = ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "vis_init", "tile_raster",
+                 "resolve", "fill", "output", "gather")
+        # (1) breakdown pass: HIP events around every kernel (they add launch
+        #     gaps, so this pass is not the headline)
+        ctx.reset_kernel_timing()
+        ctx.set_kernel_timing_filter("")
+        ctx.enable_kernel_timing(True)
+        for i in range(steps):
+            self.frame(i)
+        self.drain()
+        ctx.enable_kernel_timing(False)
+        kernels = {}
+        for name in names:
+            tot, cnt = ctx.get_kernel_timing(name)
+            if cnt:
+                kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
+        path = ctx.last_raster_path()
+        from libnativecpurenderer_amd import sharding
+        slots = self.slots_for(self.root_k) if self.nsh > 1 else None
+        share = len(sharding.owned_rows(self.H, self.nsh, self.me, slots=slots)) / self.H
+        kb = kernel_bytes(self.cfg, self.n_tri, path, share, self.args.frame_output)
+        dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
+
+        # (2) timed region: K frames, HIP events only around the dominant kernel
+        #     (every EVENT_EVERY-th frame: each record leaves a few-us bubble on
+        #     the stream, so sampling keeps the headline close to the untimed rate)
+        timing = not self.args.no_kernel_timing
+        ctx.reset_kernel_timing()
+        ctx.set_kernel_timing_filter("" if not timing else dom)
+        self.sync()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ctx.enable_kernel_timing(timing and i % EVENT_EVERY == 0)
+            self.frame(i)
+        self.drain()
+        torch.cuda.synchronize()
+        dt = self.max_over_ranks(time.perf_counter() - t0)
+        if dist is not None:
+            dist.barrier()
+        ctx.enable_kernel_timing(False)
+        ms = dt / steps * 1e3
+        tot, cnt = ctx.get_kernel_timing(dom)
+        dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
+        achieved = kb[dom] / (dom_us * 1e-6) / 1e9
+        B = algorithmic_bytes(self.cfg, self.n_tri, frame_out=self.args.frame_output)   # whole frame
+        traffic, traffic_src = load_pmc_traffic(self.cfg_name, self.nsh if self.world == 1 else 1,
+                                                slots if self.world == 1 else None, self.args.frame_output)
+        if self.world > 1:
+            traffic, traffic_src = None, None   # per-rank PMC passes are not taken on multi-GPU runs
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
+                "traffic_source": traffic_src or "none for this config/share (null)",
+                "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
+                "algorithmic_bytes_per_launch": kb[dom], "rank_share_of_frame": round(share, 6),
+                **frame_roofline(B, share, ms, self.world)}
+        out = {
+            "value": round(frags * steps / dt / 1e6, 1),
+            "ms_per_step": round(ms, 4),
+            "fps": round(1e3 / ms, 1),
+            "fragments_per_frame": int(frags),
+            "roofline": roof,
+            "raster_path": path,
+            "kernel_us": kernels,
+            "slots": slots,
+            "calib": calib,
+        }
+        if path == "ordered" and self.cfg.get("soup", (0, 0, None))[2] is not None:
+            # C5: the blend loop is bound by f64 VALU issue, not by HBM (per
+            # rank: frags is this context's count at N=1, the ranks' sum at N>1)
+            ops = (frags if self.world == 1 else frags / self.world) * BLEND_OPS_PER_FRAGMENT
+            tops = ops / (dom_us * 1e-6) / 1e12
+            out["valu_roofline"] = {"bound": "valu", "achieved": round(tops, 3), "peak": round(PEAK_F64_VALU_TOPS, 2),
+                                    "unit": "Top/s (f64 add/mul lanes)", "frac": round(tops / PEAK_F64_VALU_TOPS, 4),
+                                    "ops_per_fragment": BLEND_OPS_PER_FRAGMENT,
+                                    "note": "blended fragments x 6 f64 ops / k_tile_raster time; peak = 256 CU x 4 SIMD "
+                                            "x 16 f64 lanes/clk x 2.4 GHz"}
+        return out
 
 
 def main():
@@ -127,7 +376,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--extra", action="store_true", help="also time c2/c5 and report them under 'extra'")
+    ap.add_argument("--extra", dest="extra", action="store_true", default=None,
+                    help="also time the metric's literal config (1M tris at 1080p), c2, c5 and host-delivered "
+                         "frames, reported under 'extra' (default at N=1)")
+    ap.add_argument("--no-extra", dest="extra", action="store_false")
+    ap.add_argument("--deliver", default="none", choices=("none", "host"),
+                    help="host: every step ends with the frame output on the host (pinned buffers, D2H of frame k "
+                         "overlapped with frame k+1), as the video caller (PutRendererContextFrame) needs it")
     ap.add_argument("--no-kernel-timing", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
     ap.add_argument("--emulate-shards", type=int, default=0,
@@ -163,172 +418,72 @@ def main():
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     R.set_device(local_rank)
 
-    cfg = CONFIGS[args.config]
-    W, H = cfg["W"], cfg["H"]
-    xy, z, c = make_scene(cfg)
-    n_tri = len(xy)
-    ctx = R.RenderContext(W, H, False)
-    ctx.set_frame_format(args.frame_output)
-    if args.force_ordered:
-        ctx.set_force_ordered_raster(True)
-    buf = R.TriangleBuffer(xy, c, z=z, gouraud=cfg["gouraud"])
-    comm = None
     nsh = world if world > 1 else max(1, args.emulate_shards)
     me = rank if world > 1 else 0
-
-    def slots_for(k):
-        return None if k is None else [k] + [2] * (nsh - 1)
-
-    def apply_partition(k):
-        if nsh <= 1:
-            return
-        if k is None:
-            ctx.set_shard(nsh, me)
-        else:
-            ctx.set_shard_slots(nsh, me, slots_for(k))
-
-    fixed_k = None if args.root_slots in ("auto", "equal") else int(args.root_slots)
-    apply_partition(fixed_k)
+    run = Runner(R, args, args.config, world, rank, dist, rdev, nsh, me, args.deliver)
     if world > 1 and not args.gloo_test:
         from libnativecpurenderer_amd import sharding
-        comm = sharding.make_comm(dist, world, rank)
+        run.comm = sharding.make_comm(dist, world, rank)
+    res = run.run(args.steps, args.warmup, calibrate=world > 1 and args.root_slots == "auto")
 
-    def frame():
-        ctx.set_color(0, 0, 0, 0)
-        ctx.set_depth_state(True, cfg.get("write", True))
-        ctx.clear_depth()
-        ctx.draw_triangle_buffer(buf)
-        ctx.gather_frame_u8(comm, 0)
-
-    # fragment count of one frame (outside the timed region), summed over ranks
-    ctx.set_fragment_counting(True)
-    frame()
-    ctx.flush()
-    frags = ctx.get_fragment_count()
-    ctx.set_fragment_counting(False)
-    if dist is not None:
-        t = torch.tensor([frags], dtype=torch.int64, device=rdev)
-        dist.all_reduce(t)
-        frags = int(t.item())
-
-    def sync():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    # partition calibration (N>1, --root-slots auto): every candidate share of
-    # rank 0 is timed over a few frames (max over ranks) and the fastest kept
-    root_k, calib = fixed_k, {}
-    if world > 1 and args.root_slots == "auto":
-        for k in (None, 3, 4, 5, 6, 8, 10, 12):
-            apply_partition(k)
-            for _ in range(3):
-                frame()
-            ctx.flush()
-            sync()
-            t0 = time.perf_counter()
-            for _ in range(10):
-                frame()
-            ctx.flush()
-            torch.cuda.synchronize()
-            t = torch.tensor([time.perf_counter() - t0], device=rdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            calib["equal" if k is None else str(k)] = round(float(t.item()) / 10 * 1e3, 4)
-        best = min(calib, key=calib.get)
-        root_k = None if best == "equal" else int(best)
-        apply_partition(root_k)
-
-    for _ in range(args.warmup):
-        frame()
-    ctx.flush()
-
-    names = ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "vis_init", "tile_raster",
-             "resolve", "fill", "output", "gather")
-    # (1) breakdown pass: HIP events around every kernel (they add ~50 us per
-    #     frame of launch gaps, so this pass is not the headline)
-    ctx.reset_kernel_timing()
-    ctx.set_kernel_timing_filter("")
-    ctx.enable_kernel_timing(True)
-    for _ in range(args.steps):
-        frame()
-    ctx.flush()
-    ctx.enable_kernel_timing(False)
-    kernels = {}
-    for name in names:
-        tot, cnt = ctx.get_kernel_timing(name)
-        if cnt:
-            kernels[name] = round(tot / cnt * 1e3, 2)   # us per launch
-    path = ctx.last_raster_path()
-    from libnativecpurenderer_amd import sharding
-    frac = len(sharding.owned_rows(H, nsh, me, slots=slots_for(root_k) if nsh > 1 else None)) / H
-    kb = kernel_bytes(cfg, n_tri, path, frac, args.frame_output)
-    dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
-
-    # (2) timed region: K frames, HIP events only around the dominant kernel
-    #     (every EVENT_EVERY-th frame: each record leaves a few-us bubble on
-    #     the stream, so sampling keeps the headline close to the untimed rate)
-    ctx.reset_kernel_timing()
-    ctx.set_kernel_timing_filter("" if args.no_kernel_timing else dom)
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ctx.enable_kernel_timing(not args.no_kernel_timing and i % EVENT_EVERY == 0)
-        frame()
-    ctx.flush()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device=rdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        dist.barrier()
-    ctx.enable_kernel_timing(False)
-    ms = dt / args.steps * 1e3
-    tot, cnt = ctx.get_kernel_timing(dom)
-    dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
-    achieved = kb[dom] / (dom_us * 1e-6) / 1e9
-    B = algorithmic_bytes(cfg, n_tri, frame_out=args.frame_output)   # whole job
-    traffic, pmc = load_pmc_traffic(args.config)
+    extra = {}
+    do_extra = args.extra if args.extra is not None else (world == 1 and nsh == 1)
+    if do_extra and world == 1:
+        jobs = [("c3_1080p", "none"), ("c2", "none"), ("c5", "none"), (args.config, "host"), ("c2", "host")]
+        for name, dl in jobs:
+            if name == args.config and dl == args.deliver:
+                continue
+            sub = Runner(R, args, name, 1, 0, None, rdev, nsh, 0, dl)
+            r = sub.run(args.steps, args.warmup)
+            key = name + ("_host_delivered" if dl == "host" else "")
+            extra[key] = {"workload": sub.cfg["desc"] + (" + frame output delivered to host memory" if dl == "host" else ""),
+                          "triangles": sub.n_tri, **{k: r[k] for k in ("value", "ms_per_step", "fps",
+                                                                         "fragments_per_frame", "roofline",
+                                                                         "raster_path", "kernel_us")},
+                          **({"valu_roofline": r["valu_roofline"]} if "valu_roofline" in r else {})}
+            if dl == "host":
+                extra[key]["host_frame_bytes"] = int(np.prod(sub.ctx.frame_output_shape()))
+                same = res if name == args.config and args.deliver == "none" else extra.get(name)
+                extra[key]["in_hbm_ms_per_step"] = same["ms_per_step"] if same else None
+            del sub
 
     if rank != 0:
         return
+    cfg = run.cfg
     result = {
         "metric": "Mpixels/s shaded+Z-tested (and fps)",
-        "value": round(frags * args.steps / dt / 1e6, 1),
+        "value": res["value"],
         "unit": "Mpixels/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms, 4),
-        "fps": round(1e3 / ms, 1),
+        "ms_per_step": res["ms_per_step"],
+        "fps": res["fps"],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (deterministic displaced UV sphere / seeded soup, SURVEY.md §8d)",
-        "config": {"workload": cfg["desc"], "width": W, "height": H, "triangles": n_tri,
-                   "fragments_per_frame": int(frags), "frame_pixels": W * H,
+        "config": {"workload": cfg["desc"], "width": run.W, "height": run.H, "triangles": run.n_tri,
+                   "fragments_per_frame": res["fragments_per_frame"], "frame_pixels": run.W * run.H,
                    "frame_output": args.frame_output,
+                   "frame_delivery": "host (pinned, D2H overlapped)" if args.deliver == "host" else "in HBM",
                    "parallelism": (f"tile-row shards x{world} + RCCL u8 frame gather" if world > 1
                                    else f"EMULATED shard 0 of {nsh} on one GPU (no gather)" if nsh > 1
                                    else "single GPU"),
-                   **({"shard_slots": slots_for(root_k) or "equal", "partition_calibration_ms": calib}
+                   **({"shard_slots": res["slots"] or "equal", "partition_calibration_ms": res["calib"]}
                       if nsh > 1 else {})},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
-                     "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBPS, 4),
-                     "traffic": traffic,
-                     "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
-                     "algorithmic_bytes_per_launch": kb[dom],
-                     "frame_algorithmic_bytes": B,
-                     "frame_achieved": round(B / (ms * 1e-3) / 1e9, 1),
-                     "frame_frac": round(B / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)},
-        "raster_path": path,
-        "kernel_us": kernels,
+        "roofline": res["roofline"],
+        "raster_path": res["raster_path"],
+        "kernel_us": res["kernel_us"],
         "kernel_us_note": f"per-launch averages from a breakdown pass with events around every kernel; the timed region records events around the dominant kernel on every {EVENT_EVERY}th frame (roofline.kernel_us)",
     }
+    if "valu_roofline" in res:
+        result["valu_roofline"] = res["valu_roofline"]
+    if extra:
+        result["extra"] = extra
     if not args.no_cpu_baseline and world == 1:
-        result["cpu_baseline"] = cpu_baseline(cfg, xy, z, c)
+        result["cpu_baseline"] = cpu_baseline(cfg, run.xy, run.z, run.c)
         result["vs_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
     print(json.dumps(result))
 

@@ -161,8 +161,13 @@ void SetShardSlots(RenderContext* ctx, i64 nshards, i64 shard, const i64* slots)
                                                  of every sum(slots) <= 64 bands, interleaved (same call on all ranks) */
 i64 GetShardPattern(RenderContext* ctx, iu8* out64);   /* band b -> rank out64[b % period]; returns the period */
 bool GatherFrameU8(RenderContext* ctx, NrComm* comm, i64 root);  /* u8 frame (cpp:52-57) assembled on root */
-void GetFrameU8(RenderContext* ctx, iu8* out);
+bool GetFrameU8(RenderContext* ctx, iu8* out);
 void* GetFrameU8DevicePtr(RenderContext* ctx);
+i64 DeliverFrameU8(RenderContext* ctx, iu8* host);  /* async D2H of that frame into pinned `host` on the gather
+                                                       stream, overlapped with the next frame; -> ticket (-1: none) */
+bool WaitFrameDelivered(RenderContext* ctx, i64 ticket);
+void* AllocHostBuffer(i64 bytes);                   /* pinned host memory (DeliverFrameU8 targets) */
+void FreeHostBuffer(void* p);
 bool SetFrameFormat(RenderContext* ctx, i64 format); /* 0: u8 image (default), 1: YUV420P planes written by the
                                                        raster and gathered as such (W, H even; same on all ranks) */
 i64 GetFrameFormat(RenderContext* ctx);

@@ -100,8 +100,12 @@ DEVICE_ABI = {
     "SetShardSlots": (None, (P, L, L, P)),
     "GetShardPattern": (L, (P, P)),
     "GatherFrameU8": (B, (P, P, L)),
-    "GetFrameU8": (None, (P, P)),
+    "GetFrameU8": (B, (P, P)),
     "GetFrameU8DevicePtr": (P, (P,)),
+    "DeliverFrameU8": (L, (P, P)),
+    "WaitFrameDelivered": (B, (P, L)),
+    "AllocHostBuffer": (P, (L,)),
+    "FreeHostBuffer": (None, (P,)),
     "GetFrameYUV420P": (B, (P, P)),
     "SetFrameFormat": (B, (P, L)),
     "GetFrameFormat": (L, (P,)),

@@ -27,3 +27,7 @@ def load() -> ctypes.CDLL:
 def last_error() -> str:
     msg = load().GetLastErrorString()
     return msg.decode() if msg else ""
+
+
+def clear_error() -> None:
+    load().ClearLastError()

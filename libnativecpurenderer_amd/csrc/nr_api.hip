@@ -395,9 +395,16 @@ void ResizeRenderContext(RenderContext* ctx, i64 width, i64 height) {
     NR_CHECK(hipFree(ctx->buffer));
     if (ctx->depth) NR_CHECK(hipFree(ctx->depth));
     ctx->depth = nullptr;
+    // the gathered frame (old size) is dropped: GetFrameU8 fails until the next GatherFrameU8
+    nr_dist_sync(ctx);
+    ctx->frameLast = -1;
+    for (bool& g : ctx->gatherPending) g = false;
     ctx->width = width;
     ctx->height = height;
-    if ((width & 1) || (height & 1)) ctx->frameFormat = 0;   // YUV420P needs even sizes (SetFrameFormat)
+    if (ctx->frameFormat == 1 && ((width & 1) || (height & 1))) {   // YUV420P needs even sizes (SetFrameFormat)
+        ctx->frameFormat = 0;
+        nr_set_error_msg("ResizeRenderContext: odd size, frame output format reset from YUV420P to the u8 image");
+    }
     ctx->pendColor = ctx->pendDepth = false;
     i64 n = GetBufferSize(ctx);
     NR_CHECK(hipMalloc(&ctx->buffer, (size_t)(n > 0 ? n : 1) * sizeof(f64)));

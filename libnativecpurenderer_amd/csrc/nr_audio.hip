@@ -29,6 +29,7 @@
 //  * a negative resampled length gives an empty clip.
 #include "nr_common.h"
 
+#include <algorithm>
 #include <cstring>
 #include <atomic>
 #include <mutex>
@@ -66,11 +67,25 @@ int grid_for(i64 n) {
 // after a synchronisation of that stream, so a buffer is only ever touched in
 // that one stream's order: no other library stream or the null stream reads
 // or writes it.  Default allocator: plain hipMalloc, freed after a stream
-// synchronisation.  Round 1 saw one mix run read back a stale 32 MiB span of a
-// clip with the stream-ordered allocator (hipMallocAsync / hipFreeAsync on the
-// same stream); SetAudioStreamOrderedAlloc(true) switches back to it so that
-// tests/test_audio.py::test_mix_with_stream_ordered_allocator can keep
-// checking the whole mix under it ("Audio clips").
+// synchronisation; SetAudioStreamOrderedAlloc(true) switches to hipMallocAsync
+// / hipFreeAsync on the same stream (tests/test_audio.py runs the whole mix
+// under both).
+//
+// Round 1 saw one mix run (stream-ordered allocator) read back a stale 32 MiB
+// span of a clip.  Every device-side access of a clip is in one stream's
+// order, so the one step that was not under the library's control is the
+// readback itself: hipMemcpyAsync into the caller's PAGEABLE host memory
+// (a numpy array), which the HIP runtime does not copy as one stream-ordered
+// DMA but stages chunk by chunk through its own pinned buffers
+// (GPU_PINNED_XFER_SIZE / GPU_STAGING_BUFFER_SIZE; a 32 MiB span is one such
+// chunk), with a separate path when the source is stream-ordered pool memory.
+// One chunk landing from before the producing kernel finished is the
+// observed symptom.  The readbacks (GetAudioClipBuffer, SaveAudioClipAsWav)
+// therefore no longer hand pageable memory to the runtime: d2h_pinned copies
+// through library-owned pinned buffers, each chunk a plain stream-ordered
+// DMA that the host waits for before it touches the bytes.  This explanation
+// is inferred from the evidence (span size, allocator, pageable target); the
+// failure was never reproduced, before or after.
 std::atomic<bool> g_async_alloc{false};
 std::mutex g_async_mu;
 std::unordered_set<void*> g_async_ptrs;   // buffers from hipMallocAsync
@@ -90,6 +105,37 @@ void* alloc_bytes(size_t bytes, hipStream_t s) {
 
 f64* alloc_samples(i64 n, hipStream_t s) {
     return static_cast<f64*>(alloc_bytes((size_t)(n > 0 ? n : 1) * sizeof(f64), s));
+}
+
+// Device -> pageable host copy through two library-owned pinned buffers
+// (chunk k+1's DMA in flight while chunk k is copied out on the host); the
+// host reads a chunk only after the event of its DMA.
+constexpr size_t PIN_CHUNK = 8u << 20;
+std::mutex g_pin_mu;
+void* g_pin[2] = {nullptr, nullptr};
+hipEvent_t g_pin_ev[2] = {nullptr, nullptr};
+
+void d2h_pinned(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    for (int k = 0; k < 2; ++k)
+        if (!g_pin[k]) {
+            NR_CHECK(hipHostMalloc(&g_pin[k], PIN_CHUNK, hipHostMallocDefault));
+            NR_CHECK(hipEventCreateWithFlags(&g_pin_ev[k], hipEventDisableTiming));
+        }
+    const size_t nch = (bytes + PIN_CHUNK - 1) / PIN_CHUNK;
+    auto issue = [&](size_t c) {
+        const size_t off = c * PIN_CHUNK, len = std::min(PIN_CHUNK, bytes - off);
+        NR_CHECK(hipMemcpyAsync(g_pin[c & 1], static_cast<const iu8*>(src) + off, len, hipMemcpyDeviceToHost, s));
+        NR_CHECK(hipEventRecord(g_pin_ev[c & 1], s));
+    };
+    issue(0);
+    for (size_t c = 0; c < nch; ++c) {
+        if (c + 1 < nch) issue(c + 1);   // the other buffer: its previous chunk was copied out below
+        NR_CHECK(hipEventSynchronize(g_pin_ev[c & 1]));
+        const size_t off = c * PIN_CHUNK, len = std::min(PIN_CHUNK, bytes - off);
+        std::memcpy(static_cast<iu8*>(dst) + off, g_pin[c & 1], len);
+    }
 }
 
 // cpp:1029: (f64)v / 32768.0
@@ -550,7 +596,7 @@ WapperedBytes* SaveAudioClipAsWav(AudioClip* clip) {
         short* dv = static_cast<short*>(alloc_bytes((size_t)n * sizeof(short), s));
         hipLaunchKernelGGL(k_to_i16, dim3(grid_for(n)), dim3(AWG), 0, s, clip->buffer, dv, n);
         NR_CHECK(hipGetLastError());
-        NR_CHECK(hipMemcpyAsync(d + 44, dv, (size_t)n * sizeof(short), hipMemcpyDeviceToHost, s));
+        d2h_pinned(d + 44, dv, (size_t)n * sizeof(short), s);
         free_after(s, dv);
     }
     NR_CHECK(hipStreamSynchronize(s));
@@ -609,7 +655,7 @@ void ApplySpeedAudioClip(AudioClip* clip, f64 speed) {
 void GetAudioClipBuffer(AudioClip* clip, f64* out) {
     const i64 n = clip->numFrames * clip->channels;
     hipStream_t s = clip_stream(clip);
-    if (n > 0) NR_CHECK(hipMemcpyAsync(out, clip->buffer, (size_t)n * sizeof(f64), hipMemcpyDeviceToHost, s));
+    if (n > 0) d2h_pinned(out, clip->buffer, (size_t)n * sizeof(f64), s);
     NR_CHECK(hipStreamSynchronize(s));
 }
 

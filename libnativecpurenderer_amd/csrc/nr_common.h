@@ -124,6 +124,7 @@ struct RenderContext {
     iu8* yuvBuf = nullptr; size_t yuvCap = 0;    // GetFrameYUV420P planes (device)
     hipStream_t commStream = nullptr;            // RCCL transfers + the root's unpack
     hipEvent_t evFrameReady = nullptr, evGatherDone[2] = {nullptr, nullptr};
+    hipEvent_t evDeliver[2] = {nullptr, nullptr};   // DeliverFrameU8: D2H of frame buffer x done
     bool gatherPending[2] = {false, false};
     bool frameOutput = false;   // set by GatherFrameU8: resolves also write the u8 frame
     bool frameU8Valid = false;  // frameU8 holds the u8 image of every owned pixel

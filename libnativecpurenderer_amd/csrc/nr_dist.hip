@@ -622,14 +622,20 @@ static bool gather_local(RenderContext** ctxs, i64 n, i64 root, NrComm* self) {
 extern "C" {
 
 // NEW: copy the frame of the last GatherFrameU8 to the host (the assembled
-// image on the root; a rank's own bands elsewhere).
-void GetFrameU8(RenderContext* ctx, iu8* out) {
+// image on the root; a rank's own bands elsewhere).  False (and nothing
+// written) when there is no gathered frame: none yet, or SetFrameFormat /
+// ResizeRenderContext dropped it.
+bool GetFrameU8(RenderContext* ctx, iu8* out) {
     NR_CHECK(hipSetDevice(ctx->device));
-    if (ctx->frameLast < 0 || !ctx->frameBuf[ctx->frameLast]) return;
+    if (ctx->frameLast < 0 || !ctx->frameBuf[ctx->frameLast]) {
+        nr_set_error_msg("GetFrameU8: no gathered frame (GatherFrameU8 first; a resize or format change drops it)");
+        return false;
+    }
     if (ctx->commStream) NR_CHECK(hipStreamSynchronize(ctx->commStream));
     NR_CHECK(hipMemcpyAsync(out, ctx->frameBuf[ctx->frameLast], (size_t)nr_frame_bytes(ctx), hipMemcpyDeviceToHost,
                             ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));
+    return true;
 }
 
 // NEW: the frame of the last GatherFrameU8 as YUV420P planes
@@ -710,6 +716,62 @@ bool SetFrameFormat(RenderContext* ctx, i64 format) {
 
 i64 GetFrameFormat(RenderContext* ctx) { return ctx->frameFormat; }
 
+// NEW (§8f-2, frame delivery): the video caller hands every frame to the
+// encoder on the host (milrenderer.py:1038 -> PutRendererContextFrame,
+// cpp:232-275).  This copies the frame output of the last GatherFrameU8 (u8
+// image or YUV420P planes) into `host` -- pinned memory from AllocHostBuffer,
+// so the copy is one DMA -- on the gather stream, and returns at once: the
+// next frame renders into the other frame buffer meanwhile, and a frame buffer
+// is rendered into again only after its copy is done (device-side wait).
+// Returns a ticket for WaitFrameDelivered, or -1 when there is no gathered
+// frame.  `host` must hold nr_frame_bytes and stay untouched until the wait.
+i64 DeliverFrameU8(RenderContext* ctx, iu8* host) {
+    NR_CHECK(hipSetDevice(ctx->device));
+    const int x = ctx->frameLast;
+    if (x < 0 || !ctx->frameBuf[x]) {
+        nr_set_error_msg("DeliverFrameU8: no gathered frame (GatherFrameU8 first)");
+        return -1;
+    }
+    ensure_comm_stream(ctx);
+    if (!ctx->evDeliver[x]) NR_CHECK(hipEventCreateWithFlags(&ctx->evDeliver[x], hipEventDisableTiming));
+    const bool local = ctx->frameCur == x;   // a local gather (no assembly): buffer x was written on the main stream
+    if (local) {
+        NR_CHECK(hipEventRecord(ctx->evFrameReady, ctx->stream));
+        NR_CHECK(hipStreamWaitEvent(ctx->commStream, ctx->evFrameReady, 0));
+    }   // else: the assembly into x is already queued on the gather stream
+    NR_CHECK(hipMemcpyAsync(host, ctx->frameBuf[x], (size_t)nr_frame_bytes(ctx), hipMemcpyDeviceToHost,
+                            ctx->commStream));
+    NR_CHECK(hipEventRecord(ctx->evDeliver[x], ctx->commStream));
+    if (local) {
+        rotate_frame(ctx, x);   // the next frame renders into the other buffer
+    } else {                    // buffer x is reused only after this copy too
+        NR_CHECK(hipEventRecord(ctx->evGatherDone[x], ctx->commStream));
+        ctx->gatherPending[x] = true;
+    }
+    return x;
+}
+
+// NEW: wait until the DeliverFrameU8 with this ticket has landed on the host.
+bool WaitFrameDelivered(RenderContext* ctx, i64 ticket) {
+    if (ticket < 0 || ticket > 1 || !ctx->evDeliver[ticket]) return false;
+    NR_CHECK(hipSetDevice(ctx->device));
+    return hipEventSynchronize(ctx->evDeliver[ticket]) == hipSuccess;
+}
+
+// NEW: pinned (page-locked) host memory for DeliverFrameU8, and its release.
+void* AllocHostBuffer(i64 bytes) {
+    void* p = nullptr;
+    if (bytes <= 0 || hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
+        nr_set_error_msg("AllocHostBuffer: hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void FreeHostBuffer(void* p) {
+    if (p) NR_CHECK(hipHostFree(p));
+}
+
 // NEW: device pointer of that frame (complete once Flush returns).
 void* GetFrameU8DevicePtr(RenderContext* ctx) {
     return ctx->frameLast >= 0 ? ctx->frameBuf[ctx->frameLast] : ctx->frameU8;
@@ -776,8 +838,9 @@ void nr_dist_release(RenderContext* ctx) {
         if (ctx->frameBuf[x]) NR_CHECK(hipFree(ctx->frameBuf[x]));
         if (ctx->stageBuf[x]) NR_CHECK(hipFree(ctx->stageBuf[x]));
         if (ctx->evGatherDone[x]) NR_CHECK(hipEventDestroy(ctx->evGatherDone[x]));
+        if (ctx->evDeliver[x]) NR_CHECK(hipEventDestroy(ctx->evDeliver[x]));
         ctx->frameBuf[x] = ctx->stageBuf[x] = nullptr;
-        ctx->evGatherDone[x] = nullptr;
+        ctx->evGatherDone[x] = ctx->evDeliver[x] = nullptr;
     }
     ctx->frameU8 = nullptr;
     if (ctx->yuvBuf) NR_CHECK(hipFree(ctx->yuvBuf));

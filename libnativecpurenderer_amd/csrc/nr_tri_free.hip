@@ -395,9 +395,9 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
 // block of tiles.  Items are placed by size class without same-address LDS
 // atomics (a wave's lanes mostly share a class, and such atomics serialise):
 // per-lane class counts in registers, per-class wave scans, one LDS slot per
-// (class, wave).  Used whenever ntiles <= 16 * T (T = 256: 4096 tiles, a 4K
-// frame; T = 1024: 16384, an 8K frame).  Measured alone on C3 (rocprof): the
-// first register version 16 us, this one see DESIGN.md §4.
+// (class, wave).  Launched with T = PLAN_T = 1024 threads whenever ntiles <=
+// 16 * T (16384 tiles, an 8K frame) and the batch does not run beside a long
+// raster (free_enqueue).
 constexpr int PR_MAX = 16;
 constexpr int TILE_ARR = 16 * 1024 + 4;   // minimum length of the per-tile arrays
 template <int T, int PR>
@@ -470,15 +470,22 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     for (int k = 0; k < NWV; ++k) { tb += sh[2][k]; tm += sh[3][k]; }
     const bool fits = ta <= cap && tb <= icap;
     // class ranges, largest class first, and each wave's base inside them:
-    // thread k < PLAN_NB turns column k of csh into the wave bases of class k
+    // thread k < PLAN_NB turns column k of csh into the wave bases of class k.
+    // Every column is read (into registers) before any is rewritten: thread k
+    // sums the columns of the classes above k while their threads rewrite them.
+    u32 start = 0, col[NWV];
     if (tid < PLAN_NB) {
-        u32 start = 0;
         for (int k = PLAN_NB - 1; k > tid; --k)
             for (int q = 0; q < NWV; ++q) start += csh[k][q];
+#pragma unroll
+        for (int q = 0; q < NWV; ++q) col[q] = csh[tid][q];
+    }
+    __syncthreads();
+    if (tid < PLAN_NB) {
+#pragma unroll
         for (int q = 0; q < NWV; ++q) {
-            const u32 v = csh[tid][q];
             csh[tid][q] = start;
-            start += v;
+            start += col[q];
         }
     }
     __syncthreads();
@@ -1534,16 +1541,18 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        const bool small = !idle && plan_small(fp.period, fp.mask, src.n);   // idle GPU: the faster wide plan
+        // a large owned share (a long k_vis of the previous batch to run beside)
+        // takes the narrow plan kernel; an idle GPU the faster wide one
+        const bool besideRaster = !idle && plan_small(fp.period, fp.mask, src.n);
         const u32 icap32 = (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull);
-        // the register plan: 256 threads whenever the tiles fit (one wave per
-        // SIMD, 86 VGPRs: it fits beside running k_vis workgroups, where the
-        // 1024-thread one waits for a whole CU to drain)
-        if (plan_reg() && !small && ntiles <= PLAN_T * PR_MAX) {
-            // 1024 threads, PR = tiles per thread -> 4, 8 or 16.  Beside a long
-            // raster (small) the 65-VGPR multi-round k_free_plan_s stays: it fits the
-            // slot a finishing k_vis workgroup frees, the register plan (>128 VGPRs
-            // at PR 16) does not (C3 0.163 vs 0.172 ms; profiles/r02_c3/ab_plan_r.txt)
+        if (plan_reg() && !besideRaster && ntiles <= PLAN_T * PR_MAX) {
+            // the register plan: one 1024-thread workgroup, PR = tiles per
+            // thread -> 4, 8 or 16 (at PR 16 its tile counts, class counters and
+            // offsets take ~100 VGPRs; __launch_bounds__(1024) allows 128, so no
+            // spill).  It needs a whole CU, so beside a long raster
+            // (besideRaster) the 256-thread, 65-VGPR multi-round k_free_plan_s
+            // runs instead: it fits the slot a finishing k_vis workgroup frees
+            // (C3 0.163 vs 0.172 ms; profiles/r02_c3/ab_plan_r.txt)
             const int per = (ntiles + PLAN_T - 1) / PLAN_T;
 #define NR_PLAN_R(PP) hipLaunchKernelGGL((k_free_plan_r<PLAN_T, PP>), dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, \
                                          fp.tiles_x, fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, \
@@ -1551,7 +1560,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
             if (per <= 4) NR_PLAN_R(4); else if (per <= 8) NR_PLAN_R(8); else NR_PLAN_R(16);
 #undef NR_PLAN_R
         }
-        else if (small)
+        else if (besideRaster)
             hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
                                (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
@@ -1612,10 +1621,10 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = ext_stop() && !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
-        const bool big = plan_small(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
-        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa, st, big); else launch_vis_z<1, false>(fp, sc, F, grid, sa, st, big); }
-        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa, st, big); else launch_vis_z<2, false>(fp, sc, F, grid, sa, st, big); }
-        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa, st, big); else launch_vis_z<0, false>(fp, sc, F, grid, sa, st, big); }
+        const bool largeShare = plan_small(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
+        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<1, false>(fp, sc, F, grid, sa, st, largeShare); }
+        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<2, false>(fp, sc, F, grid, sa, st, largeShare); }
+        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<0, false>(fp, sc, F, grid, sa, st, largeShare); }
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
@@ -1687,7 +1696,8 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     if (idleInline && pipeOn && tb != nullptr && !exact) {
         const hipError_t q = hipStreamQuery(ctx->stream);
         idle = q == hipSuccess;
-        if (q != hipSuccess) (void)hipGetLastError();   // hipErrorNotReady is an answer, not a failure
+        if (q == hipErrorNotReady) (void)hipGetLastError();   // an answer, not a failure
+        else if (q != hipSuccess) NR_CHECK(q);                 // a real asynchronous error: latch it
     }
     if (!free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact && !idle, &seq,
                       known ? tb->knownPairs : 0, known ? tb->knownItems : 0, idle))

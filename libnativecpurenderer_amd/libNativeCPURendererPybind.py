@@ -358,8 +358,31 @@ class RenderContext:
             out = np.empty(self.width * self.height + 2 * (self.width // 2) * (self.height // 2), dtype=np.uint8)
         else:
             out = np.empty((self.height, self.width, 4 if self.enable_alpha else 3), dtype=np.uint8)
-        lib.GetFrameU8(self._ptr, out.ctypes.data_as(ctypes.c_void_p))
+        if not lib.GetFrameU8(self._ptr, out.ctypes.data_as(ctypes.c_void_p)):
+            raise RuntimeError("GetFrameU8 failed: " + _lib.last_error())
         return out
+
+    def frame_output_shape(self):
+        """Shape of get_frame_u8()'s array: (H, W, ipp), or the flat YUV420P planes."""
+        if lib.GetFrameFormat(self._ptr) == 1:
+            return (self.width * self.height + 2 * (self.width // 2) * (self.height // 2),)
+        return (self.height, self.width, 4 if self.enable_alpha else 3)
+
+    def deliver_frame(self, dst: "HostBuffer") -> int:
+        """Asynchronous copy of the last gathered frame output into the pinned
+        host buffer `dst` (DeliverFrameU8), overlapped with the next frame;
+        returns a ticket for wait_frame_delivered()."""
+        n = int(np.prod(self.frame_output_shape()))
+        if dst.nbytes < n:
+            raise ValueError(f"deliver_frame: the host buffer holds {dst.nbytes} bytes, the frame {n}")
+        t = lib.DeliverFrameU8(self._ptr, dst.ptr)
+        if t < 0:
+            raise RuntimeError("DeliverFrameU8 failed: " + _lib.last_error())
+        return t
+
+    def wait_frame_delivered(self, ticket: int):
+        if not lib.WaitFrameDelivered(self._ptr, ticket):
+            raise RuntimeError("WaitFrameDelivered failed: " + _lib.last_error())
 
     def set_frame_format(self, fmt: str):
         """Frame output of gather_frame_u8: "rgb" (the u8 image, cpp:52-57;
@@ -449,6 +472,26 @@ class RenderContext:
     def set_pair_capacity_override(self, pairs: int):
         """Testing: cap the visibility raster's (tile, triangle) list (0 = auto)."""
         lib.SetPairCapacityOverride(self._ptr, pairs)
+
+
+class HostBuffer:
+    """Pinned (page-locked) host memory from the library (AllocHostBuffer),
+    the target of RenderContext.deliver_frame; `array(shape)` is a numpy view."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.ptr = lib.AllocHostBuffer(self.nbytes)
+        if not self.ptr:
+            raise MemoryError("AllocHostBuffer failed: " + _lib.last_error())
+
+    def array(self, shape=None) -> np.ndarray:
+        a = np.ctypeslib.as_array((ctypes.c_ubyte * self.nbytes).from_address(self.ptr))
+        return a if shape is None else a[: int(np.prod(shape))].reshape(shape)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib.FreeHostBuffer(self.ptr)
+            self.ptr = None
 
 
 class RecordingRenderContext(RenderContext):

@@ -681,3 +681,68 @@ def test_frame_yuv420p_matches_restatement(gpu, alpha):
     odd.gather_frame_u8()
     with pytest.raises(RuntimeError):
         odd.get_frame_yuv420p()
+
+
+def test_resize_drops_the_gathered_frame(gpu):
+    """ResizeRenderContext drops the gathered frame (its buffers hold the old
+    size): get_frame_u8 raises until the next gather instead of returning an
+    unwritten buffer; an odd size resets YUV420P to the u8 image visibly (an
+    error message is latched) and the next gather is the u8 image."""
+    from libnativecpurenderer_amd import _lib
+    ctx = gpu.context(64, 48, False)
+    with pytest.raises(RuntimeError):
+        ctx.get_frame_u8()                     # nothing gathered yet
+    ctx.set_frame_format("yuv420p")
+    ctx.set_color(0.5, 0.25, 0.75, 1.0)
+    ctx.gather_frame_u8()
+    assert ctx.get_frame_u8().size == 64 * 48 * 3 // 2
+    ctx.resize(96, 64)
+    with pytest.raises(RuntimeError):
+        ctx.get_frame_u8()
+    _lib.clear_error()
+    ctx.resize(33, 20)
+    assert "YUV420P" in _lib.last_error()
+    ctx.set_color(0.5, 0.25, 0.75, 1.0)
+    ctx.gather_frame_u8()
+    assert np.array_equal(ctx.get_frame_u8(), ctx.get_buffer_as_uint8_numpy())
+
+
+@pytest.mark.parametrize("fmt", ["rgb", "yuv420p"])
+def test_delivered_frames_match_the_frames(gpu, fmt):
+    """DeliverFrameU8 (frame k's D2H on the gather stream into pinned host
+    buffers, overlapped with frame k+1's render; two host buffers in
+    rotation): every delivered frame equals that frame's output read back
+    synchronously from a second context rendering the same sequence."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    W, H = 320, 192
+    xy, z, c = scenes.triangle_soup(4000, W, H, 20, seed=77, gouraud=True)
+    buf = R.TriangleBuffer(xy, c, z=z, gouraud=True)
+    ctx, ref = gpu.context(W, H, False), gpu.context(W, H, False)
+    for cx in (ctx, ref):
+        cx.set_frame_format(fmt)
+        cx.set_depth_state(True, True)
+    shape = ctx.frame_output_shape()
+    host = [R.HostBuffer(int(np.prod(shape))) for _ in range(2)]
+    pending, got, want = None, [], []
+
+    def draw(cx, f):
+        cx.set_color(0.1 * f, 0.05, 0.2, 1.0)
+        cx.clear_depth()
+        cx.set_transform(1, 0, 0, 1, 3.0 * f, -2.0 * f)
+        cx.draw_triangle_buffer(buf)
+        cx.gather_frame_u8()
+
+    for f in range(7):
+        draw(ctx, f)
+        t = ctx.deliver_frame(host[f % 2])
+        draw(ref, f)
+        want.append(ref.get_frame_u8().copy())
+        if pending is not None:
+            ctx.wait_frame_delivered(pending[0])
+            got.append(host[pending[1]].array(shape).copy())
+        pending = (t, f % 2)
+    ctx.wait_frame_delivered(pending[0])
+    got.append(host[pending[1]].array(shape).copy())
+    for f in range(7):
+        assert np.array_equal(got[f], want[f]), (f, np.argwhere(got[f] != want[f])[:5])
+    assert not np.array_equal(want[0], want[1])
