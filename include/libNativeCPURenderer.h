@@ -150,6 +150,7 @@ i64 GetLastRasterPath(RenderContext* ctx);                               /* NEW:
 void SetForceOrderedRaster(RenderContext* ctx, bool on);                 /* NEW: A/B and tests */
 void SetPairCapacityOverride(RenderContext* ctx, i64 pairs);             /* NEW: tests (0 = automatic) */
 void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW: k_vis variant 0 auto, 1 coop, 2 lane-only */
+void SetSplitLimits(RenderContext* ctx, i64 splitAt, i64 dslice);       /* NEW: dense-tile split limits (0: defaults) */
 
 /* ---- NEW: multi-GPU frames (tile-row sharding + RCCL assembly) */
 typedef struct NrComm NrComm;

@@ -37,6 +37,7 @@ struct NRState { f64 m[6]; f64 ct[4]; };
 typedef unsigned long long u64;
 struct TriScratch {
     u64* cnt = nullptr; u64* off = nullptr; size_t tri_cap = 0;          // per triangle
+    f64* orec = nullptr; size_t orec_cap = 0;   // ordered raster: per-triangle setup records (ORec doubles each)
     u32* keys[2] = {nullptr, nullptr}; u32* vals[2] = {nullptr, nullptr}; size_t pair_cap = 0;
     u32* tile_start = nullptr; u32* tile_end = nullptr; size_t tile_cap = 0;
     void* temp = nullptr; size_t temp_bytes = 0;                        // hipcub scratch
@@ -60,7 +61,8 @@ struct TriScratch {
     } fset[3];
     int fnext = 0;                          // set of the next batch
     u32* fdone = nullptr; size_t fdone_cap = 0;   // split-tile slice counters (k_vis only)
-    u64* vis = nullptr; size_t vis_cap = 0; int visNeutral = -1;
+    u64* kslot = nullptr; size_t kslot_cap = 0;   // split-tile key slots, TH*TW keys per slice (k_vis)
+    u32 lastSplit = 0;                      // split-tile slices of the last validated batch (slot estimate)
     u32 planSeq = 0;                        // sequence number of the last async plan
     u64 lastPairs = 0;                      // capacity estimate for the next batch
     u32 lastItems = 0;                      // k_vis work items of the last validated batch (grid estimate)
@@ -68,6 +70,7 @@ struct TriScratch {
     u64 lastN = 0;                          // its triangle count (k_vis variant choice)
     u64 capOverride = 0;                    // testing: force this pair capacity
     int coopMode = 0;                       // k_vis variant: 0 auto, 1 coop, 2 lane-only (SetCoopRaster)
+    u32 splitAt = 0, dslice = 0;            // dense-tile split limits (SetSplitLimits; 0: NR_SPLIT_AT / NR_DSLICE)
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
 };
 
@@ -171,7 +174,7 @@ struct TriangleBuffer {
     // a draw under the same key is sized from them and needs no validation
     bool known = false;
     BinKey knownKey;
-    u32 knownPairs = 0, knownHeavy = 0, knownItems = 0;
+    u32 knownPairs = 0, knownHeavy = 0, knownItems = 0, knownSplit = 0;
 };
 
 // host helpers shared across translation units

@@ -277,5 +277,11 @@ void SetForceOrderedRaster(RenderContext* ctx, bool on) { ctx->forceOrdered = on
 // batch's pair density), 1 with the wave-cooperative pass for large
 // triangles, 2 without it.
 void SetCoopRaster(RenderContext* ctx, i64 mode) { ctx->tri.coopMode = (int)(mode >= 0 && mode <= 2 ? mode : 0); }
+// NEW (testing / tuning): a tile of more than min(slice, splitAt) pairs is split
+// into slices of about dslice pairs (k_vis); 0 restores the defaults.
+void SetSplitLimits(RenderContext* ctx, i64 splitAt, i64 dslice) {
+    ctx->tri.splitAt = (u32)(splitAt > 0 ? splitAt : 0);
+    ctx->tri.dslice = (u32)(dslice > 0 ? dslice : 0);
+}
 
 }  // extern "C"

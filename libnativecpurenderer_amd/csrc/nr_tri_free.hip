@@ -126,28 +126,32 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
 // It also re-zeroes the tile counters for the next batch (after reading them)
 // and the emit cursors, and mirrors the totals into pinned host memory, so a
 // batch needs no memset and no copy command.
-#ifndef NR_ROW_SPLIT
-#define NR_ROW_SPLIT 0   // tiles of at least this many triangles get one item per half tile (rows) per slice; 0: off
-#endif
-__device__ __forceinline__ bool row_split(u32 c) { return NR_ROW_SPLIT > 0 && c >= (u32)NR_ROW_SPLIT; }
-__device__ __forceinline__ u32 tile_items(u32 c, bool owned, u32 slice) {
-    // slice is a power of two: the division is a shift
-    const u32 ns = c > slice ? (c + slice - 1) >> (31 - __clz(slice)) : 1u;
-    return owned ? (row_split(c) ? 2 * ns : ns) : 0u;
+// Work items of an owned tile with c pairs: one item when c <= lim (an empty
+// tile too: k_vis writes its pending clears); a dense tile (c > lim) is split
+// into ni = ceil(c / dsl) slices of equal length.  lim and dsl come from the
+// batch's slice length (plan kernels: split_limits).
+__device__ __forceinline__ u32 tile_items(u32 c, bool owned, u32 lim, u32 dsl) {
+    if (!owned) return 0u;
+    return c > lim ? (c + dsl - 1) / dsl : 1u;
 }
 // Work item k of the ni items of a tile with c pairs from list offset ea:
-// {tile, slice begin, slice end, w}, w = slices (items sharing the tile's
-// merge, low 16 bits) | row half << 16 (0: whole tile, 1: rows [0, TH/2),
-// 2: rows [TH/2, TH)).  A dense tile (row_split) has two items per slice,
-// one per half: a half-tile item rasterises only its rows, so the dense
-// tiles' items -- the critical path of k_vis -- are half as long.
-__device__ __forceinline__ uint4 tile_item(u32 tile, u32 ea, u32 c, u32 k, u32 ni, u32 slice) {
-    if (!row_split(c)) {
-        const u32 ls = ea + k * slice;
-        return make_uint4(tile, ls, min(ls + slice, ea + c), ni);
-    }
-    const u32 ls = ea + (k >> 1) * slice;
-    return make_uint4(tile, ls, min(ls + slice, ea + c), (ni == 2 ? 1u : ni) | ((1u + (k & 1u)) << 16));
+// {tile, slice begin, slice end, w}, w = ni (items sharing the tile's merge,
+// low 16 bits) | k << 16.  Slices are ceil(c / ni) long (the last one shorter,
+// never empty: ceil(c / ni) <= dsl).
+__device__ __forceinline__ uint4 tile_item(u32 tile, u32 ea, u32 c, u32 k, u32 ni) {
+    if (ni == 1) return make_uint4(tile, ea, ea + c, 1u);
+    const u32 q = (c + ni - 1) / ni;
+    const u32 ls = ea + k * q;
+    return make_uint4(tile, ls, min(ls + q, ea + c), ni | (k << 16));
+}
+// Split limits of a batch from its slice length: a tile of more than lim =
+// min(slice, split_at) pairs is split into slices of about dsl = min(lim,
+// dslice) (>= SLICE_MIN) pairs.  Splitting only the dense tiles, finer than the
+// whole-tile limit, shortens the longest work items (k_vis's critical path)
+// without splitting the many medium tiles.
+__device__ __forceinline__ void split_limits(u32 slice, u32 split_at, u32 dslice, u32& lim, u32& dsl) {
+    lim = min(slice, split_at);
+    dsl = max((u32)SLICE_MIN, min(lim, dslice));
 }
 
 // Inclusive wave scan (64 lanes) with DPP row shifts and row broadcasts
@@ -174,8 +178,8 @@ constexpr int PLAN_NB = 12;
 // laid out largest class first: k_vis workgroups take items in index order,
 // so the long ones start first and the short ones fill the tail (a longest-
 // first schedule).  Results do not depend on the order (order-free raster).
-__device__ __forceinline__ int size_class(u32 c, u32 slice) {
-    if (c > slice) return PLAN_NB - 1;
+__device__ __forceinline__ int size_class(u32 c, u32 lim) {
+    if (c > lim) return PLAN_NB - 1;
     if (c == 0) return 0;
     const int l = 31 - __clz(c);
     return 1 + (l < PLAN_NB - 3 ? l : PLAN_NB - 3);
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
                                                       u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
                                                       u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
-                                                      u32 slice_target) {
+                                                      u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
     __shared__ u32 sh[3][PLAN_W];
     __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -210,16 +214,18 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     for (int k = 0; k < PLAN_W; ++k) { ta += sh[0][k]; th += sh[1][k]; }
     u32 slice = SLICE_MIN;
     while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
+    u32 lim, dsl;
+    split_limits(slice, split_at, dslice, lim, dsl);
     __syncthreads();
     // pass 1: items (the capacity check needs the totals before any item is
     // written) and the number of items per size class
     u32 b = 0, m = 0;
     for (int i = tid; i < ntiles; i += PLAN_T) {
         const u32 c = cnt[i];
-        const u32 ni = tile_items(c, owned_row(i / tiles_x, period, mask), slice);
+        const u32 ni = tile_items(c, owned_row(i / tiles_x, period, mask), lim, dsl);
         b += ni;
-        m += c > slice ? 1u : 0u;
-        if (ni) atomicAdd(&bcnt[size_class(c, slice)], ni);
+        m += ni > 1 ? ni : 0u;
+        if (ni) atomicAdd(&bcnt[size_class(c, lim)], ni);
     }
     b = wave_scan(b, lane); m = wave_scan(m, lane);
     if (lane == 63) { sh[1][w] = b; sh[2][w] = m; }
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     u32 tb = 0, tm = 0;
 #pragma unroll
     for (int k = 0; k < PLAN_W; ++k) { tb += sh[1][k]; tm += sh[2][k]; }
-    const bool fits = ta <= cap && tb <= icap;
+    const bool fits = ta <= cap && tb <= icap && tm <= kcap;
     if (tid == 0) {   // item ranges of the classes, largest class first
         u32 base = 0;
         for (int k = PLAN_NB - 1; k >= 0; --k) { bcur[k] = base; base += bcnt[k]; }
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         u32 c = 0, ni = 0;
         if (i < ntiles) {
             c = cnt[i];
-            ni = tile_items(c, owned_row(i / tiles_x, period, mask), slice);
+            ni = tile_items(c, owned_row(i / tiles_x, period, mask), lim, dsl);
         }
         const u32 ia = wave_scan(c, lane);
         if (lane == 63) sh[0][w] = ia;
@@ -255,8 +261,8 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         if (i < ntiles) {
             off[i] = ea;
             if (fits && ni) {
-                const u32 eb = atomicAdd(&bcur[size_class(c, slice)], ni);
-                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c, k, ni, slice);
+                const u32 eb = atomicAdd(&bcur[size_class(c, lim)], ni);
+                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c, k, ni);
             }
             cnt[i] = 0;
             cur[i] = 0;
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
                                                       u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
                                                       u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
-                                                      u32 slice_target) {
+                                                      u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
     __shared__ u32 sh[3][PS_W];
     __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -311,6 +317,8 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
     for (int k = 0; k < PS_W; ++k) { ta += sh[0][k]; th += sh[1][k]; }
     u32 slice = SLICE_MIN;
     while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
+    u32 lim, dsl;
+    split_limits(slice, split_at, dslice, lim, dsl);
     __syncthreads();
     // pass 1: item totals and items per size class
     u32 b = 0, m = 0;
@@ -322,10 +330,10 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
 #pragma unroll
         for (int j = 0; j < PS; ++j) {
             if (i0 + j >= ntiles) break;
-            const u32 ni = tile_items(c[j], owned_row((i0 + j) / tiles_x, period, mask), slice);
+            const u32 ni = tile_items(c[j], owned_row((i0 + j) / tiles_x, period, mask), lim, dsl);
             b += ni;
-            m += c[j] > slice ? 1u : 0u;
-            if (ni) atomicAdd(&bcnt[size_class(c[j], slice)], ni);
+            m += ni > 1 ? ni : 0u;
+            if (ni) atomicAdd(&bcnt[size_class(c[j], lim)], ni);
         }
     }
     b = wave_scan(b, lane); m = wave_scan(m, lane);
@@ -334,7 +342,7 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
     u32 tb = 0, tm = 0;
 #pragma unroll
     for (int k = 0; k < PS_W; ++k) { tb += sh[1][k]; tm += sh[2][k]; }
-    const bool fits = ta <= cap && tb <= icap;
+    const bool fits = ta <= cap && tb <= icap && tm <= kcap;
     if (tid == 0) {
         u32 base = 0;
         for (int k = PLAN_NB - 1; k >= 0; --k) { bcur[k] = base; base += bcnt[k]; }
@@ -365,10 +373,10 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
             const int i = i0 + j;
             if (i >= ntiles) break;
             off[i] = ea;
-            const u32 ni = tile_items(c[j], owned_row(i / tiles_x, period, mask), slice);
+            const u32 ni = tile_items(c[j], owned_row(i / tiles_x, period, mask), lim, dsl);
             if (fits && ni) {
-                const u32 eb = atomicAdd(&bcur[size_class(c[j], slice)], ni);
-                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c[j], k, ni, slice);
+                const u32 eb = atomicAdd(&bcur[size_class(c[j], lim)], ni);
+                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c[j], k, ni);
             }
             cnt[i] = 0;
             cur[i] = 0;
@@ -405,7 +413,7 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
                                                    u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                    u32* __restrict__ cur, u32* __restrict__ totals,
                                                    u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
-                                                   u32 slice_target) {
+                                                   u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
     constexpr int NWV = T / 64;
     __shared__ u32 sh[4][NWV];
     __shared__ u32 csh[PLAN_NB][NWV];
@@ -437,6 +445,8 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     }
     u32 slice = SLICE_MIN;
     while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
+    u32 lim, dsl;
+    split_limits(slice, split_at, dslice, lim, dsl);
     // items per tile, per-lane totals per size class (ownership: tile row of i0 + j)
     const int ty0 = i0 / tiles_x, tx0 = i0 - ty0 * tiles_x;
     u32 b = 0, m = 0, hc[PLAN_NB];
@@ -446,10 +456,10 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
         int ty = ty0, tx = tx0;
 #pragma unroll
         for (int j = 0; j < PR; ++j) {
-            const u32 ni = (j < per && i0 + j < ntiles) ? tile_items(c[j], owned_row(ty, period, mask), slice) : 0u;
+            const u32 ni = (j < per && i0 + j < ntiles) ? tile_items(c[j], owned_row(ty, period, mask), lim, dsl) : 0u;
             b += ni;
-            m += c[j] > slice ? 1u : 0u;
-            const int cls = size_class(c[j], slice);
+            m += ni > 1 ? ni : 0u;
+            const int cls = size_class(c[j], lim);
 #pragma unroll
             for (int k = 0; k < PLAN_NB; ++k) hc[k] += cls == k ? ni : 0u;
             if (++tx == tiles_x) { tx = 0; ++ty; }
@@ -468,7 +478,7 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     u32 tb = 0, tm = 0;
 #pragma unroll
     for (int k = 0; k < NWV; ++k) { tb += sh[2][k]; tm += sh[3][k]; }
-    const bool fits = ta <= cap && tb <= icap;
+    const bool fits = ta <= cap && tb <= icap && tm <= kcap;
     // class ranges, largest class first, and each wave's base inside them:
     // thread k < PLAN_NB turns column k of csh into the wave bases of class k.
     // Every column is read (into registers) before any is rewritten: thread k
@@ -498,14 +508,14 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
             const u32 cj = c[j];
             c[j] = ea;
             const int i = i0 + j;
-            const u32 ni = (j < per && i < ntiles) ? tile_items(cj, owned_row(ty, period, mask), slice) : 0u;
-            const int cls = size_class(cj, slice);
+            const u32 ni = (j < per && i < ntiles) ? tile_items(cj, owned_row(ty, period, mask), lim, dsl) : 0u;
+            const int cls = size_class(cj, lim);
             u32 eb = 0;
 #pragma unroll
             for (int k = 0; k < PLAN_NB; ++k)
                 if (cls == k) { eb = hc[k]; hc[k] += ni; }
             if (fits)
-                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, cj, k, ni, slice);
+                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, cj, k, ni);
             ea += cj;
             if (++tx == tiles_x) { tx = 0; ++ty; }
         }
@@ -856,6 +866,55 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         }
         return;
     }
+#ifndef NR_GOURAUD_DIRECT
+#define NR_GOURAUD_DIRECT 0
+#endif
+#ifndef NR_GD_FQ
+#define NR_GD_FQ 2
+#endif
+    if constexpr (GOURAUD && NR_GOURAUD_DIRECT) {
+        // Gouraud without the winner dedup: each pixel loads its winner's
+        // source data (L1/L2-resident: a winner's pixels are neighbours) and
+        // forms the record itself, GQ pixels' loads in flight at a time.
+        constexpr int GQ = PPT < NR_GD_FQ ? PPT : NR_GD_FQ;
+        static_assert(PPT % GQ == 0, "pixel groups");
+#pragma unroll 1
+        for (int k0 = 0; k0 < PPT; k0 += GQ) {
+            u32 id[GQ];
+            RecordSrc<true> src[GQ];
+#pragma unroll
+            for (int j = 0; j < GQ; ++j) {
+                const int p = tid + (k0 + j) * NT, lx = p & (TW - 1), ly = p / TW;
+                id[j] = 0;
+                if (lx >= wlim || ly >= hlim) continue;
+                const u64 kv = key[ly * (TW + 1) + lx];
+                id[j] = (u32)kv;
+                store_depth<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx, kv);
+                if (id[j]) load_record_src<true>(fp, (i64)id[j] - 1, src[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < GQ; ++j) {
+                const int p = tid + (k0 + j) * NT, lx = p & (TW - 1), ly = p / TW;
+                if (lx >= wlim || ly >= hlim) continue;
+                const i64 px = x0 + lx, py = y0 + ly;
+                const i64 gp = py * fp.W + px;
+                if (!id[j]) {
+                    if (fp.pendColor) {
+                        const f64 v = fp.pendColorValue;
+                        store_colour(fp, gp, px, py, v, v, v, v);
+                    }
+                    continue;
+                }
+                f64 r[16];
+                build_record<true>(fp, src[j], r);
+                f64 cr, cg, cb, ca;
+                record_colour<true>(r, px, py, cr, cg, cb, ca);
+                apply_winner(fp, gp, cr, cg, cb, ca);
+                store_colour(fp, gp, px, py, cr, cg, cb, ca);
+            }
+        }
+        return;
+    }
     u32* ht = reinterpret_cast<u32*>(lds + St::HT);
     unsigned short* hidx = reinterpret_cast<unsigned short*>(lds + St::HIDX);
     u32* didx = reinterpret_cast<u32*>(lds + St::DIDX);
@@ -1027,7 +1086,6 @@ constexpr int BIG_PX = NR_BIG_PX;
 static_assert(TH <= 64, "coop raster: one lane per tile row");
 constexpr f64 COOP_PAIRS = 2.0;
 
-constexpr int NW = VWG / 64;   // waves per k_vis workgroup
 #ifndef NR_VIS_BASE_PRIO
 #define NR_VIS_BASE_PRIO 0   // wave priority of the other k_vis items (the binning kernels run at 0)
 #endif
@@ -1053,7 +1111,7 @@ constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT, int WPE = NR_VIS_WAVES_PER_EU>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
-                                             u64* __restrict__ vis, u32* __restrict__ done,
+                                             u64* __restrict__ kslot, u32* __restrict__ done,
                                              const u32* __restrict__ plan) {
     constexpr bool DEPTH = ZMODE != 0;
     constexpr int NWV = NT / 64;   // waves per workgroup
@@ -1084,9 +1142,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         __syncthreads();
         const int tile = (int)d.x;
         const u32 ls = d.y, le = d.z;
-        const u32 nsl = d.w & 0xFFFFu, half = d.w >> 16;
+        const u32 nsl = d.w & 0xFFFFu;   // slices of the tile (d.w >> 16: this item's slice)
         const bool multi = nsl > 1;
-        const int rlo = half == 2 ? TH / 2 : 0, rhi = half == 1 ? TH / 2 : TH;   // this item's rows
+        constexpr int rlo = 0;
 #if NR_HEAVY_PRIO
         // the longest work items (dense tiles' slices) set the kernel's
         // critical path: their waves win the SIMD's issue arbitration over the
@@ -1098,7 +1156,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
         const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
-        const int rcap = hlim < rhi ? hlim : rhi;   // rows [rlo, rcap) of the tile are rasterised here
+        const int rcap = hlim;   // rows [rlo, rcap) of the tile are rasterised here
         if (ls == le) {   // no triangle: only the pending clears
             for (int p = tid; p < TH * TW; p += NT) {
                 const int lx = p & (TW - 1), ly = p / TW;
@@ -1242,31 +1300,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             }
         }
         __syncthreads();
-        if (!multi) {   // the whole list was in this slice: shade now (this item's rows)
+        if (!multi) {   // the whole list was in this slice: shade now
             if (rlo < rcap)
                 shade_tile<ZMODE, GOURAUD, NT, HS>(fp, x0, y0 + rlo, wlim, rcap - rlo, key + rlo * KS, lds, nU);
             continue;
         }
-        // split tile: merge into the global keys; the last slice to finish
-        // shades the tile and puts its keys back to the neutral value.
-        // Hand-off without cache-wide fences (an agent-scope release writes
-        // back the whole L2): the keys only ever move through device-scope
-        // atomics and sc1 loads/stores, each wave drains its atomics before
-        // the barrier, and the slice counter is a relaxed device atomic.
-        // Only keys this slice changed are merged: a key still at its initial
-        // value has no triangle id in its low word (ids are t + 1 >= 1), and the
-        // initial value never beats another slice's key; a pixel no slice
-        // changed keeps the neutral global key, read back below as "no winner".
-        for (int p = tid; p < TH * TW; p += NT) {
-            const int lx = p & (TW - 1), ly = p / TW;
-            if (lx >= wlim || ly >= hlim) continue;
-            const u64 kk = key[ly * KS + lx];
-            if (!(u32)kk) continue;
-            u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-            if (ZMODE == 1) atomicMin(g, kk);
-            else atomicMax(g, kk);
+        // split tile (a dense tile's slice): the slice's keys go to its own
+        // slot of `kslot` (slot = item index: the split tiles' items come first
+        // in the item list, plan kernels), as plain agent-coherent stores -- no
+        // read-modify-write, so the slices of a tile never contend; the slice
+        // that finishes last reduces every slot of the tile (min for LESS +
+        // write, max of the ids otherwise: every slot starts from the same
+        // initial keys) into its LDS keys and shades the tile.  The hand-off
+        // needs no cache-wide fence: the slots move through agent-scope
+        // (sc1) stores and loads, each wave drains its stores before the
+        // barrier, and the slice counter is a relaxed device atomic.
+        {
+            u64* const mine = kslot + (size_t)item * (TH * TW);
+            for (int p = tid; p < TH * TW; p += NT)   // (every key: pixels past the frame edge are never shaded)
+                __hip_atomic_store(&mine[p], key[(p / TW) * KS + (p & (TW - 1))], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: this wave's atomics performed
+        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: this wave's stores performed
         __syncthreads();
         if (tid == 0) {
             const u32 prev = __hip_atomic_fetch_add(&done[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1275,14 +1330,33 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
         __syncthreads();
         if (!sLast) continue;
-        for (int p = tid; p < TH * TW; p += NT) {   // merged keys -> LDS, global keys back to neutral
-            const int lx = p & (TW - 1), ly = p / TW;
-            if (lx >= wlim || ly >= hlim) continue;
-            u64* g = vis + (y0 + ly) * fp.W + x0 + lx;
-            const u64 neutral = ZMODE == 1 ? ~0ull : 0ull;
-            const u64 gv = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            key[ly * KS + lx] = gv == neutral ? 0ull : gv;   // untouched: no winner (only the id word is read)
-            if (gv != neutral) __hip_atomic_store(g, neutral, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        {
+            // each thread reduces its PR pixels together: per slot, PR
+            // independent loads in flight (one latency round per slot, not
+            // per pixel and slot)
+            const u32 first = item - (d.w >> 16);   // the tile's first slice (its slot)
+            constexpr int PR = TH * TW / NT;
+            u64 kk[PR];
+#pragma unroll
+            for (int j = 0; j < PR; ++j) {
+                const int p = tid + j * NT;
+                kk[j] = key[(p / TW) * KS + (p & (TW - 1))];
+            }
+            for (u32 sl = 0; sl < nsl; ++sl) {
+                if (first + sl == item) continue;
+                const u64* slot = kslot + (size_t)(first + sl) * (TH * TW);
+                u64 v[PR];
+#pragma unroll
+                for (int j = 0; j < PR; ++j)
+                    v[j] = __hip_atomic_load(slot + tid + j * NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int j = 0; j < PR; ++j) kk[j] = ZMODE == 1 ? (v[j] < kk[j] ? v[j] : kk[j]) : (v[j] > kk[j] ? v[j] : kk[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < PR; ++j) {
+                const int p = tid + j * NT;
+                key[(p / TW) * KS + (p & (TW - 1))] = kk[j];
+            }
         }
         __syncthreads();
         shade_tile<ZMODE, GOURAUD, NT, HS>(fp, x0, y0, wlim, hlim, key, lds, nU);
@@ -1338,22 +1412,22 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::F
     if (wide) {
         if (coop)
             hipExtLaunchKernelGGL((k_vis<Z, false, G, true, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, nullptr, stop, 0, fp, F.fitems,
-                               F.flist, sc.vis, sc.fdone, F.dplan);
+                               F.flist, sc.kslot, sc.fdone, F.dplan);
         else
             hipExtLaunchKernelGGL((k_vis<Z, false, G, false, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, nullptr, stop, 0, fp, F.fitems,
-                               F.flist, sc.vis, sc.fdone, F.dplan);
+                               F.flist, sc.kslot, sc.fdone, F.dplan);
     } else if (!C && vis_wpe3(big)) {
         if (coop)
             hipExtLaunchKernelGGL((k_vis<Z, false, G, true, VWG, 3>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp,
-                                  F.fitems, F.flist, sc.vis, sc.fdone, F.dplan);
+                                  F.fitems, F.flist, sc.kslot, sc.fdone, F.dplan);
         else
             hipExtLaunchKernelGGL((k_vis<Z, false, G, false, VWG, 3>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp,
-                                  F.fitems, F.flist, sc.vis, sc.fdone, F.dplan);
+                                  F.fitems, F.flist, sc.kslot, sc.fdone, F.dplan);
     } else if (coop) {
-        hipExtLaunchKernelGGL((k_vis<Z, C, G, true, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.vis,
+        hipExtLaunchKernelGGL((k_vis<Z, C, G, true, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.kslot,
                            sc.fdone, F.dplan);
     } else {
-        hipExtLaunchKernelGGL((k_vis<Z, C, G, false, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.vis,
+        hipExtLaunchKernelGGL((k_vis<Z, C, G, false, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.kslot,
                            sc.fdone, F.dplan);
     }
 }
@@ -1396,13 +1470,14 @@ static BinKey bin_key(const BinParams& bp) {
     return k;
 }
 
-static void record_known(TriangleBuffer* tb, const BinKey& key, u32 pairs, u32 heavy, u32 items) {
+static void record_known(TriangleBuffer* tb, const BinKey& key, u32 pairs, u32 heavy, u32 items, u32 split) {
     if (!tb) return;
     tb->known = true;
     tb->knownKey = key;
     tb->knownPairs = pairs;
     tb->knownHeavy = heavy;
     tb->knownItems = items;
+    tb->knownSplit = split;
 }
 
 // Items the plan kernel aims for when it picks the slice length
@@ -1413,6 +1488,28 @@ static u32 slice_target() {
         const long x = e ? atol(e) : 0;
         return x > 0 ? (u32)x : (u32)NR_SLICE_TARGET;
     }();
+    return v;
+}
+
+// Split limits of dense tiles (split_limits): NR_SPLIT_AT (a tile of more
+// pairs than min(slice, this) is split) and NR_DSLICE (its slices' length).
+#ifndef NR_SPLIT_AT
+#define NR_SPLIT_AT 1024
+#endif
+#ifndef NR_DSLICE
+#define NR_DSLICE 1024
+#endif
+static u32 env_u32(const char* name, u32 dflt) {
+    const char* e = getenv(name);
+    const long x = e ? atol(e) : 0;
+    return x > 0 ? (u32)x : dflt;
+}
+static u32 split_at() {
+    static const u32 v = env_u32("NR_SPLIT_AT", NR_SPLIT_AT);
+    return v;
+}
+static u32 dslice() {
+    static const u32 v = env_u32("NR_DSLICE", NR_DSLICE);
     return v;
 }
 
@@ -1442,7 +1539,7 @@ static hipEvent_t sync_event() {
 // batch's k_vis (only for immutable inputs: a TriangleBuffer).
 static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
                          bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0,
-                         u32 knownItems = 0, bool idle = false) {
+                         u32 knownItems = 0, bool idle = false, u32 knownSplit = 0) {
     hipStream_t sa = ctx->stream;
     hipStream_t sb = pipelined ? nr_bin_stream_for(ctx->device) : sa;
     TriScratch& sc = ctx->tri;
@@ -1479,18 +1576,17 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         F.h_plan[4] = 0;
         NR_CHECK(hipHostGetDevicePointer((void**)&F.d_hplan, F.h_plan, 0));
     }
-    u64* vb[1] = {sc.vis};
-    const size_t oldvis = sc.vis_cap;
-    if (!grow_set(vb, &sc.vis_cap, (size_t)(ctx->width * ctx->height))) return false;
-    sc.vis = vb[0];
-    // keys of split tiles merge into `vis`, which every batch leaves at the
-    // neutral value of its depth mode; refill only when the mode changes
-    const int neutral = zmode == 1 ? 1 : 0;
-    if (sc.vis_cap != oldvis || sc.visNeutral != neutral) {
-        NR_CHECK(hipMemsetD32Async((hipDeviceptr_t)sc.vis, neutral ? 0xFFFFFFFFu : 0u, sc.vis_cap * 2, sa));
-        sc.visNeutral = neutral;
-    }
-
+    // key slots of split tiles' slices (TH * TW keys each): sized from the
+    // last validated batch; the plan kernel checks the capacity on the device
+    auto grow_kslot = [&](size_t slices) {
+        slices = std::max<size_t>(slices, 1);
+        if (sc.kslot_cap >= slices * (TH * TW) && sc.kslot) return true;
+        NR_CHECK(hipStreamSynchronize(sa));   // the running raster may still read them
+        u64* kb[1] = {sc.kslot};
+        const bool ok = grow_set(kb, &sc.kslot_cap, slices * (TH * TW));
+        sc.kslot = kb[0];
+        return ok;
+    };
     auto grow_list = [&](size_t need) {
         need = std::max<size_t>(need, 1);
         if (F.flist_cap < need) quiesce();
@@ -1520,9 +1616,11 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         if (!sc.capOverride) cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
         // work items: at most one per tile + one per full slice of the list,
         // twice that with dense tiles split into row halves (NR_ROW_SPLIT)
-        if (!grow_items((NR_ROW_SPLIT > 0 ? 2 : 1) * ((size_t)ntiles + cap / SLICE_MIN + 2))) return false;
+        if (!grow_items((size_t)ntiles + cap / SLICE_MIN + 2)) return false;
+        if (!grow_kslot(std::max<size_t>(std::max<size_t>((size_t)sc.lastSplit + sc.lastSplit / 4, knownSplit), 1024)))
+            return false;
     } else {
-        if (!grow_list(1) || !grow_items(1)) return false;
+        if (!grow_list(1) || !grow_items(1) || !grow_kslot(std::max<u32>(sc.lastSplit, 1))) return false;
         cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
     }
 
@@ -1545,6 +1643,8 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         // takes the narrow plan kernel; an idle GPU the faster wide one
         const bool besideRaster = !idle && plan_small(fp.period, fp.mask, src.n);
         const u32 icap32 = (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull);
+        const u32 kcap32 = (u32)std::min<size_t>(sc.kslot_cap / (TH * TW), 0xFFFFFFF0ull);
+        const u32 sat = sc.splitAt ? sc.splitAt : split_at(), dsl = sc.dslice ? sc.dslice : dslice();
         if (plan_reg() && !besideRaster && ntiles <= PLAN_T * PR_MAX) {
             // the register plan: one 1024-thread workgroup, PR = tiles per
             // thread -> 4, 8 or 16 (at PR 16 its tile counts, class counters and
@@ -1556,18 +1656,18 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
             const int per = (ntiles + PLAN_T - 1) / PLAN_T;
 #define NR_PLAN_R(PP) hipLaunchKernelGGL((k_free_plan_r<PLAN_T, PP>), dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, \
                                          fp.tiles_x, fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, \
-                                         (u32)cap, icap32, seq, slice_target())
+                                         (u32)cap, icap32, seq, slice_target(), kcap32, sat, dsl)
             if (per <= 4) NR_PLAN_R(4); else if (per <= 8) NR_PLAN_R(8); else NR_PLAN_R(16);
 #undef NR_PLAN_R
         }
         else if (besideRaster)
             hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
-                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
+                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target(), kcap32, sat, dsl);
         else
             hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
-                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target());
+                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target(), kcap32, sat, dsl);
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_SCAN, e0, e1, sb);
 
@@ -1594,10 +1694,11 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         sc.lastPairs = F.h_plan[0];
         sc.lastHeavy = F.h_plan[5];
         sc.lastItems = F.h_plan[1];
+        sc.lastSplit = F.h_plan[2];
         sc.lastN = (u64)src.n;
         grid = F.h_plan[1];
         if (F.h_plan[3]) break;
-        if (attempt > 0 || !grow_list(F.h_plan[0]) || !grow_items(F.h_plan[1])) {
+        if (attempt > 0 || !grow_list(F.h_plan[0]) || !grow_items(F.h_plan[1]) || !grow_kslot(F.h_plan[2])) {
             nr_set_error_msg("triangle binning: pair list allocation failed");
             return false;
         }
@@ -1675,6 +1776,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         sc.lastPairs = tb->knownPairs;
         sc.lastHeavy = tb->knownHeavy;
         sc.lastItems = tb->knownItems;
+        sc.lastSplit = tb->knownSplit;
     }
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % bin_sets();
@@ -1700,10 +1802,10 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         else if (q != hipSuccess) NR_CHECK(q);                 // a real asynchronous error: latch it
     }
     if (!free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact && !idle, &seq,
-                      known ? tb->knownPairs : 0, known ? tb->knownItems : 0, idle))
+                      known ? tb->knownPairs : 0, known ? tb->knownItems : 0, idle, known ? tb->knownSplit : 0))
         return;
     if (exact) {
-        record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems);
+        record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems, sc.lastSplit);
     } else if (!known) {
         PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq, tb, key};
         ctx->pendingBatch = pb;
@@ -1744,7 +1846,8 @@ void settle(RenderContext* ctx) {
     sc.lastPairs = F.h_plan[0];
     sc.lastHeavy = F.h_plan[5];
     sc.lastItems = F.h_plan[1];
-    record_known(pb->tb, pb->key, F.h_plan[0], F.h_plan[5], F.h_plan[1]);   // exact totals, fitted or not
+    sc.lastSplit = F.h_plan[2];
+    record_known(pb->tb, pb->key, F.h_plan[0], F.h_plan[5], F.h_plan[1], F.h_plan[2]);   // exact totals, fitted or not
     if (!F.h_plan[3]) {
         // overflow: the batch's later kernels did nothing; re-run it exactly
         // on the main stream, after everything queued so far

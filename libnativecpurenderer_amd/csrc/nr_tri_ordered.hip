@@ -27,7 +27,39 @@ constexpr int NWAVE = TH / RPW;  // 8
 constexpr int WG = NWAVE * 64;   // 512 threads
 constexpr int CH = 64;           // triangles staged per chunk
 
-__global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt) {
+// Per-triangle setup record of the ordered raster, formed once per triangle
+// by k_tri_count (a triangle of C5 lies in ~100 tiles; the raster used to set
+// it up again in each): screen vertices, edge slopes, 1/den, depths and the
+// depth-pass bound (zpass_bound).  16 doubles, 128 B, 16-B aligned.
+enum { R_X0 = 0, R_Y0, R_X1, R_Y1, R_X2, R_Y2, R_SL0, R_SL1, R_SL2, R_INV, R_Z0, R_Z1, R_Z2, R_FLAGS, ORec = 16 };
+
+// Depth-pass proof (zpass_all): with the Z test on and Z write off, a
+// triangle passes the LESS test on every pixel the exact span rule covers when
+// all of them quantise (nr_quantize_depth) strictly below the tile's smallest
+// depth zmin.  For a triangle with G = max|edge| / |den|, bbox extent S and
+// coordinate magnitude M, G*S <= 1e4 and G*M <= 1e4 bound the computed
+// barycentrics of covered pixels to [-1e-10, 1 + 1e-10] (span-rule crossings
+// and the w1/w2 expressions both err by O(u (G S + G M)), u = 2^-53; den's
+// cancellation by O(u G S) relative), so with |z| <= 2 the computed depth is at
+// most max(z) + 1e-9 (< max(z) + 1e-8, the bound used).  The triangle-only
+// part is this bound, quantised, or 0xFFFFFFFF when the analysis does not
+// apply (no tile minimum lies above it): zpass_all == (zpass_bound < zmin).
+__device__ __forceinline__ u32 zpass_bound(const f64 (&sx)[3], const f64 (&sy)[3], f64 e1x, f64 e1y, f64 e2x, f64 e2y,
+                                           f64 den, f64 z0, f64 z1, f64 z2) {
+    if (!tri_finite(sx, sy) || den == 0) return 0xFFFFFFFFu;
+    if (!(fabs(z0) <= 2 && fabs(z1) <= 2 && fabs(z2) <= 2)) return 0xFFFFFFFFu;   // (NaN: no bound)
+    const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
+    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+    const f64 e = fmax(fmax(fabs(e1x), fabs(e1y)), fmax(fabs(e2x), fabs(e2y)));
+    const f64 G = e / fabs(den);
+    const f64 S = (xmx - xmn) + (ymx - ymn) + 4.0;
+    const f64 M = fmax(fmax(fabs(xmn), fabs(xmx)), fmax(fabs(ymn), fabs(ymx))) + 1.0;
+    if (!(G * S <= 1e4 && G * M <= 1e4)) return 0xFFFFFFFFu;
+    return nr_quantize_depth(fmax(fmax(z0, z1), z2) + 1e-8);
+}
+
+__global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt,
+                                                   f64* __restrict__ rec) {
     const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
     if (t >= bp.src.n) return;
     f64 sx[3], sy[3];
@@ -40,6 +72,23 @@ __global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned 
         c = (unsigned long long)(tx1 - tx0 + 1) * rows;
     }
     cnt[t] = c;
+    if (!c) return;   // never listed: no record needed
+    const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+    const f64 den = e1x * e2y - e2x * e1y;
+    f64 sl[3];
+    edge_slopes(sx, sy, sl);
+    f64 z0 = 0, z1 = 0, z2 = 0;
+    if (bp.src.z) { z0 = bp.src.z[t * 3]; z1 = bp.src.z[t * 3 + 1]; z2 = bp.src.z[t * 3 + 2]; }
+    // (tri_tiles lists only finite triangles with den != 0: valid)
+    const u64 flags = 1ull | ((u64)zpass_bound(sx, sy, e1x, e1y, e2x, e2y, den, z0, z1, z2) << 32);
+    double2* r = reinterpret_cast<double2*>(rec + t * ORec);
+    r[0] = make_double2(sx[0], sy[0]);
+    r[1] = make_double2(sx[1], sy[1]);
+    r[2] = make_double2(sx[2], sy[2]);
+    r[3] = make_double2(sl[0], sl[1]);
+    r[4] = make_double2(sl[2], 1.0 / den);
+    r[5] = make_double2(z0, z1);
+    r[6] = make_double2(z2, __longlong_as_double((long long)flags));
 }
 
 __global__ __launch_bounds__(256) void k_tri_emit(const BinParams bp, const unsigned long long* __restrict__ off,
@@ -73,28 +122,6 @@ __device__ __forceinline__ u32 wave_min_u32(u32 v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v = min(v, (u32)__shfl_xor((int)v, d, 64));
     return v;
-}
-
-// True when every pixel the exact span rule covers quantises (nr_quantize_depth)
-// strictly below zmin, so the LESS test passes on all of them.  For a
-// triangle with G = max|edge| / |den|, bbox extent S and coordinate magnitude
-// M, G*S <= 1e4 and G*M <= 1e4 bound the computed barycentrics of covered
-// pixels to [-1e-10, 1 + 1e-10] (span-rule crossings and the w1/w2
-// expressions both err by O(u (G S + G M)), u = 2^-53; den's cancellation by
-// O(u G S) relative), so with |z| <= 2 the computed depth is at most
-// max(z) + 1e-9 (< max(z) + 1e-8, the bound used).  Anything else: false.
-__device__ __forceinline__ bool zpass_all(const f64 (&sx)[3], const f64 (&sy)[3], f64 e1x, f64 e1y, f64 e2x, f64 e2y,
-                                          f64 den, f64 z0, f64 z1, f64 z2, u32 zmin) {
-    if (!tri_finite(sx, sy) || den == 0) return false;
-    if (!(fabs(z0) <= 2 && fabs(z1) <= 2 && fabs(z2) <= 2)) return false;   // (NaN: false)
-    const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
-    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
-    const f64 e = fmax(fmax(fabs(e1x), fabs(e1y)), fmax(fabs(e2x), fabs(e2y)));
-    const f64 G = e / fabs(den);
-    const f64 S = (xmx - xmn) + (ymx - ymn) + 4.0;
-    const f64 M = fmax(fmax(fabs(xmn), fabs(xmx)), fmax(fabs(ymn), fabs(ymx))) + 1.0;
-    if (!(G * S <= 1e4 && G * M <= 1e4)) return false;
-    return nr_quantize_depth(fmax(fmax(z0, z1), z2) + 1e-8) < zmin;
 }
 
 // LDS staging slots of a chunk (SoA, CH entries each)
@@ -137,7 +164,8 @@ __device__ __forceinline__ bool span_lane(u64 sp, int r) {   // this lane in row
 // stores alpha, so the per-fragment alpha moves are dropped.
 template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
-                                                    const u32* __restrict__ tstart, const u32* __restrict__ tend) {
+                                                    const u32* __restrict__ tstart, const u32* __restrict__ tend,
+                                                    const f64* __restrict__ rec) {
     const int tile = blockIdx.x;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
     const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
@@ -200,29 +228,27 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
     for (u32 base = ls; base < le; base += CH) {
         const int cnt = (le - base) < (u32)CH ? (int)(le - base) : CH;
-        // ---- (a) triangle setup, one thread per triangle
+        // ---- (a) triangle setup, one thread per triangle: the record
+        // k_tri_count formed (zpass_bound) and the per-tile parts
         if (tid < cnt) {
             const i64 t = list[base + tid];
-            f64 sx[3], sy[3];
-            tri_screen(fp.src, fp.m, t, sx, sy);
+            const double2* r = reinterpret_cast<const double2*>(rec + t * ORec);
+            const double2 v0 = r[0], v1 = r[1], v2 = r[2], v3 = r[3], v4 = r[4];
+            const f64 sx[3] = {v0.x, v1.x, v2.x}, sy[3] = {v0.y, v1.y, v2.y};
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-            const f64 den = e1x * e2y - e2x * e1y;
-            VALID[tid] = tri_finite(sx, sy) && den != 0;
+            VALID[tid] = 1;   // (only valid triangles are listed)
             S[S_X0][tid] = sx[0]; S[S_Y0][tid] = sy[0];
             S[S_X1][tid] = sx[1]; S[S_Y1][tid] = sy[1];
             S[S_X2][tid] = sx[2]; S[S_Y2][tid] = sy[2];
             S[S_E1X][tid] = e1x; S[S_E1Y][tid] = e1y; S[S_E2X][tid] = e2x; S[S_E2Y][tid] = e2y;
-            S[S_INV][tid] = 1.0 / den;
-            {
-                f64 sl[3];
-                edge_slopes(sx, sy, sl);
-                S[S_SL0][tid] = sl[0]; S[S_SL1][tid] = sl[1]; S[S_SL2][tid] = sl[2];
-            }
+            S[S_INV][tid] = v4.y;
+            S[S_SL0][tid] = v3.x; S[S_SL1][tid] = v3.y; S[S_SL2][tid] = v4.x;
             if (DEPTH) {
-                f64 z0 = 0, z1 = 0, z2 = 0;
-                if (fp.src.z) { z0 = fp.src.z[t * 3]; z1 = fp.src.z[t * 3 + 1]; z2 = fp.src.z[t * 3 + 2]; }
+                const double2 v5 = r[5], v6 = r[6];
+                const f64 z0 = v5.x, z1 = v5.y, z2 = v6.x;
                 S[S_Z0][tid] = z0; S[S_DZ1][tid] = z1 - z0; S[S_DZ2][tid] = z2 - z0;
-                ZPASS[tid] = !fp.depthWrite && zpass_all(sx, sy, e1x, e1y, e2x, e2y, den, z0, z1, z2, zTileMin);
+                const u32 zb = (u32)((u64)__double_as_longlong(v6.y) >> 32);
+                ZPASS[tid] = !fp.depthWrite && zb < zTileMin;   // zpass_all
             }
             if (GOURAUD) {
                 const f64* c = fp.src.rgba + t * 12;
@@ -297,8 +323,39 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             // every triangle of the chunk: ApplyPixel from the per-triangle
             // terms on the covered lanes (a loop with one path, so the pixel
             // registers are updated in place)
-            // (only the triangles touching this wave's rows)
-            for (; hm; hm &= hm - 1) {
+            // (only the triangles touching this wave's rows).  Software
+            // pipelined: the next triangle's span word and blend terms are
+            // read from LDS while this one blends, so the LDS latency is not
+            // on the loop's dependency chain.
+#ifndef NR_BLEND_PIPE
+#define NR_BLEND_PIPE 0   // 1: measured slower on C5 (859 vs 821 us, profiles/r03_c5/ab_blend_pipe.txt)
+#endif
+            if (NR_BLEND_PIPE && hm) {
+                int k = (int)__builtin_ctzll(hm);
+                u64 spv = SP[k][wave];
+                f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
+                f64 fA = RGBA ? S[S_FA][k] : 0.0;
+                for (;;) {
+                    hm &= hm - 1;
+                    const int kn = hm ? (int)__builtin_ctzll(hm) : k;
+                    const u64 spn = SP[kn][wave];
+                    const f64 omn = S[S_OM][kn], RAn = S[S_RA][kn], GAn = S[S_GA][kn], BAn = S[S_BA][kn];
+                    const f64 fAn = RGBA ? S[S_FA][kn] : 0.0;
+                    const u64 sp = uniform_u64(spv);
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        if (span_lane(sp, r)) {
+                            cr[r] = cr[r] * om + RA;
+                            cg[r] = cg[r] * om + GA;
+                            cb[r] = cb[r] * om + BA;
+                            if (RGBA) ca[r] = fA;
+                        }
+                    }
+                    if (!hm) break;
+                    spv = spn; om = omn; RA = RAn; GA = GAn; BA = BAn; fA = fAn;
+                }
+            }
+            for (; !NR_BLEND_PIPE && hm; hm &= hm - 1) {
                 const int k = (int)__builtin_ctzll(hm);
                 const u64 spv = SP[k][wave];
                 const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
@@ -429,19 +486,20 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 }
 
 template <bool G, bool D, bool C>
-void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s) {
-    if (fp.ipp == 4) hipLaunchKernelGGL((k_tile_raster<G, D, C, true>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te);
-    else hipLaunchKernelGGL((k_tile_raster<G, D, C, false>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te);
+void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s,
+                   const f64* rec) {
+    if (fp.ipp == 4) hipLaunchKernelGGL((k_tile_raster<G, D, C, true>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te, rec);
+    else hipLaunchKernelGGL((k_tile_raster<G, D, C, false>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te, rec);
 }
 
 template <bool C>
 void launch_raster_c(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles,
-                     hipStream_t s) {
+                     hipStream_t s, const f64* rec) {
     const bool g = fp.src.gouraud != 0, d = fp.depthTest != 0;
-    if (g && d) launch_raster<true, true, C>(fp, list, ts, te, ntiles, s);
-    else if (g) launch_raster<true, false, C>(fp, list, ts, te, ntiles, s);
-    else if (d) launch_raster<false, true, C>(fp, list, ts, te, ntiles, s);
-    else launch_raster<false, false, C>(fp, list, ts, te, ntiles, s);
+    if (g && d) launch_raster<true, true, C>(fp, list, ts, te, ntiles, s, rec);
+    else if (g) launch_raster<true, false, C>(fp, list, ts, te, ntiles, s, rec);
+    else if (d) launch_raster<false, true, C>(fp, list, ts, te, ntiles, s, rec);
+    else launch_raster<false, false, C>(fp, list, ts, te, ntiles, s, rec);
 }
 
 }  // namespace
@@ -461,6 +519,9 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
     u64* tri_bufs[2] = {sc.cnt, sc.off};
     if (!grow_set(tri_bufs, &sc.tri_cap, (size_t)src.n)) return;
     sc.cnt = tri_bufs[0]; sc.off = tri_bufs[1];
+    f64* rec_bufs[1] = {sc.orec};
+    if (!grow_set(rec_bufs, &sc.orec_cap, (size_t)std::max<i64>(src.n, 1) * ORec)) return;
+    sc.orec = rec_bufs[0];
     u32* tile_bufs[2] = {sc.tile_start, sc.tile_end};
     if (!grow_set(tile_bufs, &sc.tile_cap, (size_t)ntiles)) return;
     sc.tile_start = tile_bufs[0]; sc.tile_end = tile_bufs[1];
@@ -468,7 +529,7 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
     const int g1 = (int)((src.n + 255) / 256);
     hipEvent_t e0, e1;
     nr_timing_begin(ctx, NRK_TRI_COUNT, &e0, &e1);
-    hipLaunchKernelGGL(k_tri_count, dim3(g1), dim3(256), 0, s, bp, sc.cnt);
+    hipLaunchKernelGGL(k_tri_count, dim3(g1), dim3(256), 0, s, bp, sc.cnt, sc.orec);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TRI_COUNT, e0, e1);
 
@@ -532,8 +593,8 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
     }
 
     nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-    if (fp.fragCounter) launch_raster_c<true>(fp, list, sc.tile_start, sc.tile_end, ntiles, s);
-    else launch_raster_c<false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s);
+    if (fp.fragCounter) launch_raster_c<true>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
+    else launch_raster_c<false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
     ctx->lastPath = 2;

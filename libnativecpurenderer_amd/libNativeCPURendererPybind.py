@@ -469,6 +469,11 @@ class RenderContext:
         pass for large triangles, 2 lane-per-triangle only."""
         lib.SetCoopRaster(self._ptr, mode)
 
+    def set_split_limits(self, split_at: int = 0, dslice: int = 0):
+        """Testing / tuning: tiles of more than min(slice, split_at) pairs are
+        split into slices of about `dslice` pairs (0: the defaults)."""
+        lib.SetSplitLimits(self._ptr, split_at, dslice)
+
     def set_pair_capacity_override(self, pairs: int):
         """Testing: cap the visibility raster's (tile, triangle) list (0 = auto)."""
         lib.SetPairCapacityOverride(self._ptr, pairs)

@@ -746,3 +746,35 @@ def test_delivered_frames_match_the_frames(gpu, fmt):
     for f in range(7):
         assert np.array_equal(got[f], want[f]), (f, np.argwhere(got[f] != want[f])[:5])
     assert not np.array_equal(want[0], want[1])
+
+
+@pytest.mark.parametrize("limits", [(64, 64), (200, 96), (512, 256)])
+def test_split_dense_tiles_match_oracle(gpu, oracle, limits):
+    """Dense tiles split into slices (SetSplitLimits: tiles of more than
+    split_at pairs cut into slices of ~dslice pairs), each slice's keys in its
+    own slot, the last slice reducing them and shading: every depth mode, RGB
+    and RGBA, flat and Gouraud, against the oracle -- from ~1000 pairs per tile
+    (up to 16 slices a tile) down to tiles just over the limit."""
+    W, H = 256, 160
+    dense = scenes.triangle_soup(20000, W, H, 3, seed=91, gouraud=True)
+    big = scenes.triangle_soup(200, W, H, 60, seed=92, gouraud=True)
+    xy = np.concatenate([dense[0], big[0]]); z = np.concatenate([dense[1], big[1]])
+    c = np.concatenate([dense[2], big[2]])
+    perm = np.random.Generator(np.random.PCG64(93)).permutation(len(xy))
+    xy, z, c = xy[perm], z[perm], c[perm]
+    for depth, write in ((True, True), (True, False), (False, True)):
+        for alpha in (False, True):
+            for gouraud in (True, False):
+                cc = c if gouraud else c[:, :4]
+                outs = []
+                for fac in (gpu, oracle):
+                    ctx = fac.context(W, H, alpha)
+                    if fac is gpu:
+                        ctx.set_split_limits(*limits)
+                    ctx.set_color(0.25, 0.25, 0.25, 0.25)
+                    ctx.set_depth_state(depth, write)
+                    ctx.clear_depth()
+                    ctx.draw_triangles(xy, cc, z=z)
+                    ctx.draw_triangles(xy[::3] + 0.5, cc[::3], z=z[::3] * 0.5)   # a second batch over the first
+                    outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+                assert_same(outs[0], outs[1], f"split {limits} depth={depth} write={write} alpha={alpha} g={gouraud}")

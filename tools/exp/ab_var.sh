@@ -5,7 +5,7 @@ cp libnativecpurenderer_amd/libNativeCPURenderer.so /tmp/keep.so
 for r in $(seq $reps); do
   for v in "$@"; do
     cp tools/exp/$v.so libnativecpurenderer_amd/libNativeCPURenderer.so
-    timeout -k 10 120 python bench.py --no-cpu-baseline --steps 100 $args > gpurun_out/abv.json 2>&1 || { cp /tmp/keep.so libnativecpurenderer_amd/libNativeCPURenderer.so; exit 1; }
+    timeout -k 10 120 python bench.py --no-cpu-baseline --no-extra --steps 100 $args > gpurun_out/abv.json 2>&1 || { cp /tmp/keep.so libnativecpurenderer_amd/libNativeCPURenderer.so; exit 1; }
     echo "$v $args $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/abv.json) $(grep -o '"tile_raster": [0-9.]*' gpurun_out/abv.json)"
   done
 done

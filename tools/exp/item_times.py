@@ -54,7 +54,11 @@ for lo, hi in ((0, 1), (1, 64), (64, 256), (256, 512), (512, 1025)):
 m = nsl > 1
 if m.any():
     print(f"  split slices: n={m.sum():5d} dur mean {dur[m].mean():7.2f} max {dur[m].max():7.2f} us"
-          f"  us/tri {dur[m].sum() / max(1, ntri[m].sum()):.4f}")
+          f"  us/tri {dur[m].sum() / max(1, ntri[m].sum()):.4f}  tris mean {ntri[m].mean():.0f}")
+    after = np.where(tm2 > 0, tm2 / 100.0, dur)          # item start -> slot written + counter
+    last = m & (e - (s + after) > 0.5)                   # the slices that went on to shade
+    print(f"    raster {ras[m].mean():6.2f}  slot write+counter {(after[m] - ras[m]).mean():6.2f}"
+          f"  last slices {last.sum()}: reduce+shade {(e[last] - s[last] - after[last]).mean() if last.any() else 0:6.2f}")
 edges = np.arange(0, span + 2, 2.0)
 act = np.zeros(len(edges))
 for i, t in enumerate(edges):
