@@ -37,7 +37,33 @@ struct BinParams {
     int tiles_x;
     int period;           // owned tile rows: bit (ty % period) of mask (SetShard / SetShardSlots)
     u64 mask;
+    // the owned tile rows, numbered 0.. (the binning kernels' LDS histograms
+    // hold only those): pc owned slots per period, slotOf[k] = the k-th
+    // owned slot; hrows = owned rows of the frame (set_owned_rows)
+    int pc, hrows;
+    unsigned char slotOf[64];
 };
+
+// Ordinal of owned tile row ty among the owned rows, and its inverse
+// (unsharded: the identity, no division).
+__device__ __forceinline__ int owned_ord(const BinParams& bp, int ty) {
+    if (bp.period == 1) return ty;
+    const int q = ty / bp.period, s = ty - q * bp.period;
+    return q * bp.pc + __builtin_popcountll(bp.mask & ((1ull << s) - 1ull));
+}
+__device__ __forceinline__ int owned_row_of(const BinParams& bp, int ord) {
+    if (bp.period == 1) return ord;
+    const int q = ord / bp.pc;
+    return q * bp.period + bp.slotOf[ord - q * bp.pc];
+}
+inline void set_owned_rows(BinParams& bp, int tiles_y) {
+    bp.pc = 0;
+    for (int s = 0; s < bp.period && s < 64; ++s)
+        if ((bp.mask >> s) & 1ull) bp.slotOf[bp.pc++] = (unsigned char)s;
+    bp.hrows = 0;
+    for (int ty = 0; ty < tiles_y; ++ty)
+        if (bp.period == 1 || ((bp.mask >> (ty % bp.period)) & 1ull)) ++bp.hrows;
+}
 
 // (unsharded: no integer division -- it costs ~30 VALU instructions)
 __device__ __forceinline__ bool owned_row(int ty, int period, u64 mask) {
@@ -213,6 +239,95 @@ __device__ __forceinline__ void row_span_slopes(const f64 (&sx)[3], const f64 (&
     }
     xs = (int)clampd(fmin(ka, kb) - x0, 0.0, wlim);
     xe = (int)clampd(fmax(ka, kb) - x0, 0.0, wlim);
+}
+
+// ---- f32 fast path of row_span_slopes (k_vis) -----------------------------
+// The two straddling edges of a row are the two edges at the vertex alone on
+// its side of the row: the edges at the lowest-y vertex above the middle
+// vertex's y (L = min-max, T = min-mid), at the highest-y vertex from there on
+// (L, B = mid-max) -- row_span_in's selection, made once per triangle.  Each
+// crossing cc = (y - yi) * s + xi is evaluated in f32 relative to the tile
+// origin (xi - x0, yi - y0: exact in f64, small), which is cheap (f32 issues at
+// twice the f64 rate) and whose error bound is small:
+//   |cc32 - cc| <= 2^-24 (|cc| + 4|v| + |xr|) + |s| (|yr| 2^-48 + |yi| 2^-53)
+//                  + |xi| 2^-53 + (the f64 expression's own rounding, 2^-50 (|v| + |cc|))
+// (v = (y - yi) s; the bound used, eps = 2^-22 |cc32| + 2^-20 |v32| + ce, has a
+// factor 4 of margin and ce per edge).  When cc32 is further than eps from the
+// integers on both sides, ceil(cc32) is the exact expression's ceil; otherwise
+// (or for non-finite / huge values: eps or cc32 not finite) the row takes
+// row_span_slopes, which is itself exact.
+struct Edge32 {
+    float x, yhi, ylo, s, ce;   // anchor vertex relative to the tile origin (y as hi + lo), slope, error term
+};
+
+__device__ __forceinline__ Edge32 edge32(f64 xi, f64 yi, f64 s, f64 x0, f64 y0) {
+    Edge32 e;
+    const f64 xr = xi - x0, yr = yi - y0;
+    e.x = (float)xr;
+    e.yhi = (float)yr;
+    e.ylo = (float)(yr - (f64)e.yhi);
+    e.s = (float)s;
+    const float as = fabsf(e.s);
+    e.ce = fabsf(e.x) * 0x1p-21f + as * (fabsf(e.yhi) * 0x1p-46f + (float)(fabs(yi) * 0x1p-51)) +
+           (float)(fabs(xi) * 0x1p-51) + 0x1p-23f;
+    return e;
+}
+
+// Per-triangle edge selection: L (min-y vertex to max-y vertex), T (min-mid),
+// B (mid-max), each as pointInPolygon's edge k anchored at vertex k (edge_slopes);
+// ymid = the middle vertex's y (rows y < ymid use L and T, the others L and B).
+struct Span32 {
+    Edge32 L, T, B;
+    f64 ymid;
+};
+
+__device__ __forceinline__ Span32 span32_setup(const f64 (&sx)[3], const f64 (&sy)[3], const f64 (&sl)[3], f64 x0,
+                                               f64 y0) {
+    const f64 a = sy[0], b = sy[1], c = sy[2];
+    const int imin = (b < a) ? ((c < b) ? 2 : 1) : ((c < a) ? 2 : 0);
+    const int imax = (b >= a) ? ((c >= b) ? 2 : 1) : ((c >= a) ? 2 : 0);
+    const int imid = 3 - imin - imax;
+    // edge id of vertex pair {p, q}: {0,2} -> 0, {0,1} -> 1, {1,2} -> 2 (sums 2, 1, 3)
+    auto eid = [](int p, int q) { const int s = p + q; return s == 2 ? 0 : (s == 1 ? 1 : 2); };
+    auto pick = [&](int k) {
+        const f64 xi = k == 0 ? sx[0] : (k == 1 ? sx[1] : sx[2]);
+        const f64 yi = k == 0 ? sy[0] : (k == 1 ? sy[1] : sy[2]);
+        const f64 si = k == 0 ? sl[0] : (k == 1 ? sl[1] : sl[2]);
+        return edge32(xi, yi, si, x0, y0);
+    };
+    Span32 S;
+    S.L = pick(eid(imin, imax));
+    S.T = pick(eid(imin, imid));
+    S.B = pick(eid(imid, imax));
+    S.ymid = imid == 0 ? a : (imid == 1 ? b : c);
+    return S;
+}
+
+__device__ __forceinline__ float crossing32(const Edge32& e, float rf, bool& ok) {
+    const float bb = (rf - e.yhi) - e.ylo;
+    const float v = bb * e.s;
+    const float cc = v + e.x;
+    const float k = ceilf(cc);
+    const float d = k - cc;   // in [0, 1), exact
+    const float eps = fmaf(fabsf(cc), 0x1p-22f, fmaf(fabsf(v), 0x1p-20f, e.ce));
+    ok = ok && (d > eps) && ((1.0f - d) > eps);
+    return k;
+}
+
+// Row r of the tile (y = y0 + r, a row with exactly two straddling edges):
+// the span [xs, xe) relative to x0, clamped to [0, wlim], when the f32 bound
+// proves it (returns true); false: the caller evaluates row_span_slopes.
+__device__ __forceinline__ bool row_span32(const Span32& S, int r, f64 y, float wlim, int& xs, int& xe) {
+    const bool top = y < S.ymid;
+    const Edge32& E = top ? S.T : S.B;
+    const float rf = (float)r;
+    bool ok = true;
+    const float ka = crossing32(S.L, rf, ok);
+    const float kb = crossing32(E, rf, ok);
+    const float lo = fminf(ka, kb), hi = fmaxf(ka, kb);
+    xs = (int)fminf(fmaxf(lo, 0.0f), wlim);
+    xe = (int)fminf(fmaxf(hi, 0.0f), wlim);
+    return ok;
 }
 
 // State snapshot of one draw call (passed by value to the kernels).

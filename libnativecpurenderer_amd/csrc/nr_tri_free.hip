@@ -83,8 +83,10 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
         const i64 t = base + k * 256 + tid;
         if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
     }
+    // LDS histogram over the owned tile rows only (a sharded frame's share)
+    const int hbins = bp.hrows * bp.tiles_x;
     if (LDSH) {
-        for (int b = tid; b < ntiles; b += 256) hist[b] = 0;
+        for (int b = tid; b < hbins; b += 256) hist[b] = 0;
         __syncthreads();
     }
 #pragma unroll
@@ -100,18 +102,21 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
         if (!hit) continue;
         for (int ty = ty0; ty <= ty1; ++ty) {
             if (!owned_row(ty, bp.period, bp.mask)) continue;
+            const int hrow = (LDSH ? owned_ord(bp, ty) : ty) * bp.tiles_x;
             for (int tx = tx0; tx <= tx1; ++tx) {
-                const int bin = ty * bp.tiles_x + tx;
-                if (LDSH) atomicAdd(&hist[bin], 1u);
-                else atomicAdd(&tile_cnt[bin], 1u);
+                if (LDSH) atomicAdd(&hist[hrow + tx], 1u);
+                else atomicAdd(&tile_cnt[hrow + tx], 1u);
             }
         }
     }
     if (LDSH) {
         __syncthreads();
-        for (int b = tid; b < ntiles; b += 256) {
+        for (int b = tid; b < hbins; b += 256) {
             const u32 h = hist[b];
-            if (h) atomicAdd(&tile_cnt[b], h);
+            if (h) {
+                const int r = b / bp.tiles_x;
+                atomicAdd(&tile_cnt[owned_row_of(bp, r) * bp.tiles_x + (b - r * bp.tiles_x)], h);
+            }
         }
     }
 }
@@ -581,8 +586,9 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
         const i64 t = base + k * 256 + tid;
         rk[k] = t < bp.src.n ? rects[t] : NO_RECT;
     }
+    const int hbins = bp.hrows * bp.tiles_x;   // (owned tile rows only, as k_free_count)
     if (LDSH) {
-        for (int b = tid; b < ntiles; b += 256) hist[b] = 0;
+        for (int b = tid; b < hbins; b += 256) hist[b] = 0;
         __syncthreads();
         for (int k = 0; k < TPT; ++k) {
             const i64 t = base + k * 256 + tid;
@@ -592,14 +598,20 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
             const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
             const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
             for (int ty = ty0; ty <= ty1; ++ty)
-                if (owned_row(ty, bp.period, bp.mask))
-                    for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * bp.tiles_x + tx], 1u);
+                if (owned_row(ty, bp.period, bp.mask)) {
+                    const int hrow = owned_ord(bp, ty) * bp.tiles_x;
+                    for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[hrow + tx], 1u);
+                }
         }
         __syncthreads();
         // reserve each touched tile's range once: hist[b] becomes the next slot
-        for (int b = tid; b < ntiles; b += 256) {
+        for (int b = tid; b < hbins; b += 256) {
             const u32 h = hist[b];
-            if (h) hist[b] = off[b] + atomicAdd(&cur[b], h);
+            if (h) {
+                const int r = b / bp.tiles_x;
+                const int tile = owned_row_of(bp, r) * bp.tiles_x + (b - r * bp.tiles_x);
+                hist[b] = off[tile] + atomicAdd(&cur[tile], h);
+            }
         }
         __syncthreads();
     }
@@ -612,9 +624,10 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
         const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
         for (int ty = ty0; ty <= ty1; ++ty) {
             if (!owned_row(ty, bp.period, bp.mask)) continue;
+            const int hrow = (LDSH ? owned_ord(bp, ty) : ty) * bp.tiles_x;
             for (int tx = tx0; tx <= tx1; ++tx) {
-                const int bin = ty * bp.tiles_x + tx;
-                const u32 slot = LDSH ? atomicAdd(&hist[bin], 1u) : off[bin] + atomicAdd(&cur[bin], 1u);
+                const u32 slot = LDSH ? atomicAdd(&hist[hrow + tx], 1u)
+                                      : off[hrow + tx] + atomicAdd(&cur[hrow + tx], 1u);
                 list[slot] = (u32)t;
             }
         }
@@ -866,55 +879,6 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         }
         return;
     }
-#ifndef NR_GOURAUD_DIRECT
-#define NR_GOURAUD_DIRECT 0
-#endif
-#ifndef NR_GD_FQ
-#define NR_GD_FQ 2
-#endif
-    if constexpr (GOURAUD && NR_GOURAUD_DIRECT) {
-        // Gouraud without the winner dedup: each pixel loads its winner's
-        // source data (L1/L2-resident: a winner's pixels are neighbours) and
-        // forms the record itself, GQ pixels' loads in flight at a time.
-        constexpr int GQ = PPT < NR_GD_FQ ? PPT : NR_GD_FQ;
-        static_assert(PPT % GQ == 0, "pixel groups");
-#pragma unroll 1
-        for (int k0 = 0; k0 < PPT; k0 += GQ) {
-            u32 id[GQ];
-            RecordSrc<true> src[GQ];
-#pragma unroll
-            for (int j = 0; j < GQ; ++j) {
-                const int p = tid + (k0 + j) * NT, lx = p & (TW - 1), ly = p / TW;
-                id[j] = 0;
-                if (lx >= wlim || ly >= hlim) continue;
-                const u64 kv = key[ly * (TW + 1) + lx];
-                id[j] = (u32)kv;
-                store_depth<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx, kv);
-                if (id[j]) load_record_src<true>(fp, (i64)id[j] - 1, src[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < GQ; ++j) {
-                const int p = tid + (k0 + j) * NT, lx = p & (TW - 1), ly = p / TW;
-                if (lx >= wlim || ly >= hlim) continue;
-                const i64 px = x0 + lx, py = y0 + ly;
-                const i64 gp = py * fp.W + px;
-                if (!id[j]) {
-                    if (fp.pendColor) {
-                        const f64 v = fp.pendColorValue;
-                        store_colour(fp, gp, px, py, v, v, v, v);
-                    }
-                    continue;
-                }
-                f64 r[16];
-                build_record<true>(fp, src[j], r);
-                f64 cr, cg, cb, ca;
-                record_colour<true>(r, px, py, cr, cg, cb, ca);
-                apply_winner(fp, gp, cr, cg, cb, ca);
-                store_colour(fp, gp, px, py, cr, cg, cb, ca);
-            }
-        }
-        return;
-    }
     u32* ht = reinterpret_cast<u32*>(lds + St::HT);
     unsigned short* hidx = reinterpret_cast<unsigned short*>(lds + St::HIDX);
     u32* didx = reinterpret_cast<u32*>(lds + St::DIDX);
@@ -966,7 +930,22 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
     }
     __syncthreads();   // every key read: the records may overwrite them
     const u32 U = nU < (u32)St::RT ? nU : (u32)St::RT;
-    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);
+#ifndef NR_REC_Q
+#define NR_REC_Q 2
+#endif
+    if constexpr (NR_REC_Q >= 2) {
+        // two winners per thread per round, both records' loads in flight
+        for (u32 u = tid; u < U; u += 2 * NT) {
+            RecordSrc<GOURAUD> s0, s1;
+            const bool two = u + NT < U;
+            load_record_src<GOURAUD>(fp, (i64)didx[u] - 1, s0);
+            if (two) load_record_src<GOURAUD>(fp, (i64)didx[u + NT] - 1, s1);
+            build_record<GOURAUD>(fp, s0, rec + u * St::REC);
+            if (two) build_record<GOURAUD>(fp, s1, rec + (u + NT) * St::REC);
+        }
+    } else {
+        for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);
+    }
     __syncthreads();
 #pragma unroll 1
     for (int k = 0; k < PPT; ++k) {
@@ -1224,12 +1203,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             edge_slopes(sx, sy, sl);
             const f64 inv = 1.0 / den;
             const u64 id1 = (u64)t + 1;
+#ifndef NR_SPAN32
+#define NR_SPAN32 1
+#endif
+            // f32 row spans (row_span32) with the exact f64 row_span_in for the
+            // rows the f32 bound cannot decide: C2 -2 %, one rank's 8-way C3
+            // share -3 % (k_vis 44 -> 40 us); the 3-wave instance (C3) keeps the
+            // f64 spans: neutral there at +18 VGPRs (profiles/r03_c3/ab_span32.txt)
+            constexpr bool SPAN32 = NR_SPAN32 && WPE != 3;
             if (r0 < r1 && !big) {
+                Span32 S32;
+                if (SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
                 for (int r = r0; r < r1; ++r) {
                     const f64 y = (f64)(int)(y0 + r);
                     int xs, xe;
-                    row_span_slopes(sx, sy, sl, y, (f64)x0, (f64)wlim, xs, xe);
+                    if (!SPAN32) row_span_slopes(sx, sy, sl, y, (f64)x0, (f64)wlim, xs, xe);
+                    else if (!row_span32(S32, r, y, (float)wlim, xs, xe))
+                        row_span_in(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);   // (rare: the exact statement)
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
                     if (xs >= xe) continue;
                     if (ZMODE == 0) {
@@ -1624,8 +1615,9 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
     }
 
-    const bool ldsh = ntiles <= LDS_HIST_MAX;
-    const size_t hbytes = ldsh ? (size_t)ntiles * sizeof(u32) : 0;
+    const int hbins = bp.hrows * fp.tiles_x;   // LDS histograms: the owned tile rows
+    const bool ldsh = hbins <= LDS_HIST_MAX;
+    const size_t hbytes = ldsh ? (size_t)hbins * sizeof(u32) : 0;
     const int gb = (int)((src.n + 256 * TPT - 1) / (256 * TPT));
     hipEvent_t e0, e1;
     u32 grid;
@@ -1748,6 +1740,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
     bp.period = fp.period; bp.mask = fp.mask;
+    set_owned_rows(bp, fp.tiles_y);
     // fragment counting reads a counter back anyway: run exact (synchronous);
     // so does a batch from the caller's device arrays: a deferred overflow
     // re-run (settle, at the next call) could read them after the caller has

@@ -515,6 +515,7 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
     bp.period = fp.period; bp.mask = fp.mask;
+    set_owned_rows(bp, fp.tiles_y);
 
     u64* tri_bufs[2] = {sc.cnt, sc.off};
     if (!grow_set(tri_bufs, &sc.tri_cap, (size_t)src.n)) return;
