@@ -178,6 +178,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     __shared__ f64 S[S_NSLOT][CH];
     // a wave's 4 row spans of triangle k: bits 16r..16r+15 = span_word of row r
     __shared__ u64 SP[CH][NWAVE];
+#ifndef NR_LANE_MASKS
+#define NR_LANE_MASKS 1
+#endif
+    // the blend-only loop's lane masks of a wave's 4 rows of triangle k,
+    // formed by the span phase's 512 threads (VALU) instead of by each blending
+    // wave's scalar unit: that loop is bound by scalar issue
+    __shared__ __attribute__((aligned(16))) u64 SPM[NR_LANE_MASKS ? CH : 1][NWAVE][RPW];
     // span-phase ballots: HITW[w] byte g = which of triangles 8w..8w+7 touch
     // the rows of wave g (bit j: triangle 8w + j)
     __shared__ u64 HITW[NWAVE];
@@ -302,6 +309,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     sp |= (u64)span_word(xs, xe) << (16 * r);
                     touch |= xs < xe;
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
+                    if (NR_LANE_MASKS) SPM[k][rg][r] = span_lanes(span_word(xs, xe));
                 }
                 SP[k][rg] = sp;
             }
@@ -357,13 +365,22 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             }
             for (; !NR_BLEND_PIPE && hm; hm &= hm - 1) {
                 const int k = (int)__builtin_ctzll(hm);
-                const u64 spv = SP[k][wave];
                 const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
                 const f64 fA = RGBA ? S[S_FA][k] : 0.0;
-                const u64 sp = uniform_u64(spv);
+                u64 lm[RPW];
+                if (NR_LANE_MASKS) {   // the 4 rows' lane masks, formed by the span phase
+                    const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
+                    const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
+                    lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
+                    lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
+                } else {
+                    const u64 sp = uniform_u64(SP[k][wave]);
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) lm[r] = span_lanes((u32)(sp >> (16 * r)) & 0xFFFFu);
+                }
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
-                    if (span_lane(sp, r)) {
+                    if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
                         cr[r] = cr[r] * om + RA;
                         cg[r] = cg[r] * om + GA;
                         cb[r] = cb[r] * om + BA;

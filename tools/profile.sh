@@ -8,7 +8,7 @@ TAG=${2:-r01}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="$GRAFT_REPO_ROOT/bench.py --config $CFG --no-cpu-baseline"
+BENCH="$GRAFT_REPO_ROOT/bench.py --config $CFG --no-cpu-baseline --no-extra $BENCH_EXTRA"
 run() {  # name, timeout, args...
   local name=$1; shift; local t=$1; shift
   timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
