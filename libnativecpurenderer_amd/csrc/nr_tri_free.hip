@@ -1674,16 +1674,11 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
                 const char* e = getenv("NR_GRID_EST");
                 return e ? atoi(e) != 0 : true;
             }();
-            // NR_GRID_DIV = k: a workgroup takes k work items in turn (A/B)
-            static const u64 gridDiv = [] {
-                const char* e = getenv("NR_GRID_DIV");
-                const long x = e ? atol(e) : 1;
-                return (u64)(x > 1 ? x : 1);
-            }();
+            // (two or three items per workgroup in turn: C3 k_vis 138 -> 150 / 157 us,
+            // profiles/r03_c3/ab_grid_div.txt)
             u64 g = F.fitems_cap;
             if (gridEst && knownItems) g = knownItems;
             else if (gridEst && sc.lastItems) g = std::max<u64>((u64)sc.lastItems + sc.lastItems / 4, 1024);
-            g = std::max<u64>((g + gridDiv - 1) / gridDiv, std::min<u64>(g, 768));
             grid = (u32)std::min<u64>(std::min<u64>(g, F.fitems_cap), 8192);
             break;
         }

@@ -19,7 +19,7 @@ cand = [(len(v.get("FETCH_SIZE", [])), k) for k, v in vals.items() if v.get("FET
 n, k = max(cand)
 fetch = sum(vals[k]["FETCH_SIZE"]) / len(vals[k]["FETCH_SIZE"])
 write = sum(vals[k]["WRITE_SIZE"]) / len(vals[k]["WRITE_SIZE"])
-out = {"kernel": k.replace("void ", "").split("(")[0].replace("nrtri::(anonymous namespace)::", ""), "config": tag,
+out = {"kernel": k.replace("void ", "").replace("nrtri::(anonymous namespace)::", "").split("(")[0], "config": tag,
        "bench_args": args, "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
        "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "dispatches": n,
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py --steps 3 --warmup 1), "
