@@ -1165,20 +1165,34 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const u32 ns = le - ls;
         const u32 cs = ns >= 64u * NWV ? 64u : (ns + NWV - 1) / NWV;
         const u32 nch = (ns + cs - 1) / cs;
-        u32 pt = 0;
-        f64 pxy[6], pz[3] = {0, 0, 0};
-        auto prefetch = [&](u32 c) {
+        // Loads run two chunks ahead for the list and one chunk ahead for the
+        // triangle data: chunk c's setup issues the vertex loads of chunk
+        // c + NWV from an index that arrived during chunk c - NWV, and the
+        // index of chunk c + 2 NWV -- the dependent list -> vertex load pair
+        // is never waited on inside a chunk (it used to stall every chunk
+        // for one memory latency before the setup).
+        // Every load here is unconditional, from an in-range address (a lane
+        // past the chunk reads the slice's first entry, a real triangle), and
+        // nothing is computed from a loaded value until it is used: a
+        // conditional load, or a use right after it, makes the compiler wait
+        // for the loads in flight on the spot.
+        auto list_at = [&](u32 c) -> u32 {
             const u32 b = ls + c * cs + lane;
-            if (c < nch && (u32)lane < cs && b < le) {
-                pt = list[b];
-                load_tri_xy(fp.src.xy, pt, pxy);
-                if (DEPTH && fp.src.z) {
-                    const f64* qz = fp.src.z + (i64)pt * 3;
-                    pz[0] = qz[0]; pz[1] = qz[1]; pz[2] = qz[2];
-                }
+            return list[c < nch && (u32)lane < cs && b < le ? b : ls];
+        };
+        // chunk c + NWV's triangle (loaded) and chunk c + 2 NWV's (in flight)
+        u32 pt = list_at(wave), ptn = list_at(wave + NWV);
+        const bool hasZ = DEPTH && fp.src.z;
+        const f64* const zsrc = hasZ ? fp.src.z : fp.src.xy;   // (no z: any valid address, values unused)
+        f64 pxy[6], pz[3];
+        auto prefetch = [&](u32 t) {
+            load_tri_xy(fp.src.xy, t, pxy);
+            if (DEPTH) {
+                const f64* qz = zsrc + (i64)t * 3;
+                pz[0] = qz[0]; pz[1] = qz[1]; pz[2] = qz[2];
             }
         };
-        prefetch(wave);
+        prefetch(pt);
         for (u32 c = wave; c < nch; c += NWV) {
             const u32 base = ls + c * cs;
             const int cnt = (int)((le - base) < cs ? (le - base) : cs);
@@ -1186,8 +1200,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             f64 sx[3], sy[3], sl[3];
 #pragma unroll
             for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
-            const f64 zz0 = pz[0], dz1 = pz[1] - pz[0], dz2 = pz[2] - pz[0];
-            prefetch(c + NWV);
+            const f64 zz0 = hasZ ? pz[0] : 0.0;
+            const f64 dz1 = hasZ ? pz[1] - pz[0] : 0.0, dz2 = hasZ ? pz[2] - pz[0] : 0.0;
+            pt = ptn;
+            prefetch(pt);
+            ptn = list_at(c + 2 * NWV);
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
             const f64 den = e1x * e2y - e2x * e1y;
             int r0 = 0, r1 = 0;   // rows with a straddling edge: ymin <= y < ymax (exact)
