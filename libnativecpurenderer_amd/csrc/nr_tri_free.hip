@@ -281,7 +281,6 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
             __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // the batch's sequence number last: the host polls it (nr_settle)
         __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -396,6 +395,7 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
             __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the batch's sequence number last: the host polls it (nr_settle)
         __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -1227,7 +1227,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             // rows the f32 bound cannot decide: C2 -2 %, one rank's 8-way C3
             // share -3 % (k_vis 44 -> 40 us); the 3-wave instance (C3) keeps the
             // f64 spans: neutral there at +18 VGPRs (profiles/r03_c3/ab_span32.txt)
-            constexpr bool SPAN32 = NR_SPAN32 && WPE != 3;
+#ifndef NR_SPAN32_WPE3
+#define NR_SPAN32_WPE3 0
+#endif
+            constexpr bool SPAN32 = NR_SPAN32 && (WPE != 3 || NR_SPAN32_WPE3);
             if (r0 < r1 && !big) {
                 Span32 S32;
                 if (SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);

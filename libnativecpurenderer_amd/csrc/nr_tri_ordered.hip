@@ -9,8 +9,8 @@
 //                   submission order (painter's order is preserved)
 //   5 k_tile_ranges start/end of each tile's list
 //   6 k_tile_raster one 512-thread workgroup per tile; the tile's colour and
-//                   Z live in registers (8 waves x 4 rows x 64 lanes) for the
-//                   whole list.  Per 64-triangle chunk the setup and the exact
+//                   Z live in registers (8 waves, each a 32 x 8 block: 4
+//                   pixels per lane) for the whole list.  Per 64-triangle chunk the setup and the exact
 //                   per-row coverage spans are staged in LDS, then each wave
 //                   walks the chunk in order and blends its covered lanes
 //                   (ApplyPixel, cpp:529-547).  The tile is read once and
@@ -22,10 +22,25 @@
 namespace nrtri {
 namespace {
 
-constexpr int RPW = 4;           // rows per wave
-constexpr int NWAVE = TH / RPW;  // 8
+constexpr int RPW = 4;           // steps per wave: a lane holds RPW pixels of the tile in registers
+constexpr int NWAVE = 8;         // waves per tile
 constexpr int WG = NWAVE * 64;   // 512 threads
 constexpr int CH = 64;           // triangles staged per chunk
+// Wave blocks: a wave owns a block of BW columns x RPW * SR rows of the tile
+// (BW * SR = 64 lanes; step r of lane l is the pixel (l % BW, r * SR + l / BW)
+// of the block).  Square-ish blocks cut the (triangle, wave) units a large
+// triangle's edges cross: C5 needs 6.28 M units with 64 x 4 blocks, 5.09 M with
+// 32 x 8 and 4.77 M with 16 x 16 (counted from the scene on the CPU).  Measured
+// (C5 k_tile_raster): 778 us at 64 x 4, 715 us at 32 x 8, 746 us at 16 x 16 (its
+// masks take four window ballots and more span-phase work per chunk), so 32 x 8
+// (profiles/r03_c5/ab_blocks.txt).
+#ifndef NR_ORD_BW
+#define NR_ORD_BW 32
+#endif
+constexpr int BW = NR_ORD_BW;    // block columns (64, 32 or 16)
+constexpr int SR = 64 / BW;      // rows per step
+constexpr int NQ = TW / BW;      // column windows of the tile
+static_assert(BW * SR == 64 && NQ * (TH / (RPW * SR)) == NWAVE, "wave blocks tile the tile");
 
 // Per-triangle setup record of the ordered raster, formed once per triangle
 // by k_tri_count (a triangle of C5 lies in ~100 tiles; the raster used to set
@@ -144,20 +159,13 @@ __device__ __forceinline__ u64 uniform_u64(u64 v) {   // (a wave-uniform value i
            (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)v);
 }
 
-// A row's coverage span [xs, xe) within the tile as a 16-bit word:
-// xs | (64 - xe) << 8, an empty row as 63 | 1 << 8.  Its lanes as a wave mask
-// take two shifts and an AND of scalar registers (the empty row's shifts leave
-// no bit), and the mask is the lane condition itself (inverse ballot): no
-// per-lane compares.
-constexpr u32 SPAN_EMPTY = 63u | (1u << 8);
-__device__ __forceinline__ u32 span_word(int xs, int xe) {
-    return xs < xe ? (u32)xs | ((u32)(64 - xe) << 8) : SPAN_EMPTY;
-}
-__device__ __forceinline__ u64 span_lanes(u32 w16) {
-    return (~0ull << (w16 & 63u)) & (~0ull >> ((w16 >> 8) & 63u));
-}
-__device__ __forceinline__ bool span_lane(u64 sp, int r) {   // this lane in row r's span (sp: the wave's 4 rows)
-    return __builtin_amdgcn_inverse_ballot_w64(span_lanes((u32)(sp >> (16 * r)) & 0xFFFFu));
+// Bits [xs, xe) of a BW-bit window (xs, xe relative to the window, clamped).
+__device__ __forceinline__ u64 window_bits(int xs, int xe) {
+    xs = max(xs, 0);
+    xe = min(xe, BW);
+    if (xs >= xe) return 0ull;
+    const int n = xe - xs;
+    return (n == 64 ? ~0ull : ((1ull << n) - 1ull)) << xs;
 }
 
 // RGBA: the context has an alpha channel (ipp 4).  An RGB context never
@@ -176,32 +184,32 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
 
     __shared__ f64 S[S_NSLOT][CH];
-    // a wave's 4 row spans of triangle k: bits 16r..16r+15 = span_word of row r
-    __shared__ u64 SP[CH][NWAVE];
-#ifndef NR_LANE_MASKS
-#define NR_LANE_MASKS 1
-#endif
-    // the blend-only loop's lane masks of a wave's 4 rows of triangle k,
-    // formed by the span phase's 512 threads (VALU) instead of by each blending
-    // wave's scalar unit: that loop is bound by scalar issue
-    __shared__ __attribute__((aligned(16))) u64 SPM[NR_LANE_MASKS ? CH : 1][NWAVE][RPW];
-    // span-phase ballots: HITW[w] byte g = which of triangles 8w..8w+7 touch
-    // the rows of wave g (bit j: triangle 8w + j)
-    __shared__ u64 HITW[NWAVE];
+    // the lane masks of a wave's RPW steps for triangle k (bit l: lane l's
+    // pixel of that step is covered), formed by the span phase's 512 threads
+    // in VALU: the blend loop only moves them into scalar registers and sets
+    // exec (it is bound by scalar issue)
+    __shared__ __attribute__((aligned(16))) u64 SPM[CH][NWAVE][RPW];
+    // span-phase ballots, one per column window q: HITQ[q][w] byte g = which of
+    // triangles 8w..8w+7 touch window q of the tile rows 4g..4g+3
+    __shared__ u64 HITQ[NQ][NWAVE];
     __shared__ iu8 VALID[CH];
     __shared__ iu8 ZPASS[CH];   // depth test known to pass on every covered pixel (see zpass_all)
     __shared__ u32 zmin_w[NWAVE];
     __shared__ unsigned long long fragSum;
     if (COUNT && tid == 0) fragSum = 0;
 
-    // ---- the tile's pixel state, resident in registers for the whole list
-    const i64 px = x0 + lane;
+    // ---- the tile's pixel state, resident in registers for the whole list:
+    // this wave's block (band, q), the lane's column and its row in each step
+    const int band = wave / NQ, q = wave - band * NQ;
+    const int lcol = q * BW + (lane % BW);               // column in the tile
+    const int lrow0 = band * (RPW * SR) + lane / BW;     // row in the tile at step 0 (step r: + r * SR)
+    const i64 px = x0 + lcol;
     constexpr int ipp = RGBA ? 4 : 3;
     f64 cr[RPW], cg[RPW], cb[RPW], ca[RPW];
     u32 cz[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-        const i64 py = y0 + wave * RPW + r;
+        const i64 py = y0 + lrow0 + r * SR;
         cr[r] = cg[r] = cb[r] = ca[r] = 0;
         cz[r] = 0xFFFFFFFFu;
         if (px < fp.W && py < fp.H) {
@@ -283,13 +291,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             blendOnly = zok && S[S_FA][tid] != 1;
         }
         const bool allBlend = __syncthreads_and(blendOnly ? 1 : 0) != 0;
-        // ---- (b) exact coverage spans: thread = (triangle k, wave-row group rg);
-        // wave w takes triangles 8w..8w+7, lane = rg * 8 + (k - 8w), so the
-        // wave's ballot of "touches the rows" holds one byte per row group
+        // ---- (b) exact coverage spans: thread = (triangle k, row group rg =
+        // tile rows 4rg..4rg+3); wave w takes triangles 8w..8w+7, lane = rg * 8
+        // + (k - 8w).  Its 4 rows are 4 / SR steps of the waves of band rg / SR
+        // (one per column window): it writes those 4 lane masks, and the
+        // wave's ballot per window holds one byte per row group
         {
             const int k = (wave << 3) | (lane & 7), rg = lane >> 3;
-            u64 sp = 0;
-            bool touch = false;
+            bool touch[NQ];
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) touch[qq] = false;
             if (k < cnt) {
                 const bool ok = VALID[k];
                 const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
@@ -299,29 +310,50 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 // two edges straddle (row_span_slopes = row_span there); none
                 // elsewhere (row_span's empty span)
                 const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+                u64 mk[RPW];   // [j * NQ + qq]: step (4 rg % (RPW SR)) / SR + j of window qq
 #pragma unroll
-                for (int r = 0; r < RPW; ++r) {
-                    const int row = rg * RPW + r;
+                for (int i = 0; i < RPW; ++i) mk[i] = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = rg * 4 + r;
                     const i64 gy = y0 + row;
                     int xs = 0, xe = 0;
                     if (ok && gy < fp.H && ymn <= (f64)gy && (f64)gy < ymx)
                         row_span_slopes(sx, sy, sl, (f64)gy, (f64)x0, wlim, xs, xe);
-                    sp |= (u64)span_word(xs, xe) << (16 * r);
-                    touch |= xs < xe;
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
-                    if (NR_LANE_MASKS) SPM[k][rg][r] = span_lanes(span_word(xs, xe));
+#pragma unroll
+                    for (int qq = 0; qq < NQ; ++qq)
+                        mk[(r / SR) * NQ + qq] |= window_bits(xs - qq * BW, xe - qq * BW) << ((r % SR) * BW);
                 }
-                SP[k][rg] = sp;
+                const int b = rg / SR;                        // band of these rows
+                const int st0 = ((rg * 4) % (RPW * SR)) / SR; // their first step
+#pragma unroll
+                for (int j = 0; j < 4 / SR; ++j)
+#pragma unroll
+                    for (int qq = 0; qq < NQ; ++qq) {
+                        SPM[k][b * NQ + qq][st0 + j] = mk[j * NQ + qq];
+                        touch[qq] |= mk[j * NQ + qq] != 0;
+                    }
             }
-            const u64 hit = __ballot(touch);
-            if (lane == 0) HITW[wave] = hit;
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) {
+                const u64 hit = __ballot(touch[qq]);
+                if (lane == 0) HITQ[qq][wave] = hit;
+            }
         }
         __syncthreads();
-        // this wave's triangles of the chunk (bit k: triangle k touches its rows)
+        // this wave's triangles of the chunk (bit k: triangle k touches its
+        // block): the bytes of its band's SR row groups in its window's ballots
         u64 hm = 0;
 #pragma unroll
-        for (int w = 0; w < NWAVE; ++w) hm |= ((uniform_u64(HITW[w]) >> (8 * wave)) & 0xFFull) << (8 * w);
-        // ---- (c) in-order raster of the chunk; each wave owns 4 rows.
+        for (int w = 0; w < NWAVE; ++w) {
+            const u64 h = uniform_u64(HITQ[q][w]) >> (8 * band * SR);
+            u64 m = 0;
+#pragma unroll
+            for (int i = 0; i < SR; ++i) m |= h >> (8 * i);
+            hm |= (m & 0xFFull) << (8 * w);
+        }
+        // ---- (c) in-order raster of the chunk; each wave owns its block.
         // Every product of the per-pixel expressions that is constant along
         // a column (dx * e2y, dx * e1y), along a row (e2x * dy, e1x * dy) or
         // over the triangle (flat: src * colourTransform, src * a, 1 - a) is
@@ -330,54 +362,17 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (!GOURAUD && allBlend) {
             // every triangle of the chunk: ApplyPixel from the per-triangle
             // terms on the covered lanes (a loop with one path, so the pixel
-            // registers are updated in place)
-            // (only the triangles touching this wave's rows).  Software
-            // pipelined: the next triangle's span word and blend terms are
-            // read from LDS while this one blends, so the LDS latency is not
-            // on the loop's dependency chain.
-#ifndef NR_BLEND_PIPE
-#define NR_BLEND_PIPE 0   // 1: measured slower on C5 (859 vs 821 us, profiles/r03_c5/ab_blend_pipe.txt)
-#endif
-            if (NR_BLEND_PIPE && hm) {
-                int k = (int)__builtin_ctzll(hm);
-                u64 spv = SP[k][wave];
-                f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
-                f64 fA = RGBA ? S[S_FA][k] : 0.0;
-                for (;;) {
-                    hm &= hm - 1;
-                    const int kn = hm ? (int)__builtin_ctzll(hm) : k;
-                    const u64 spn = SP[kn][wave];
-                    const f64 omn = S[S_OM][kn], RAn = S[S_RA][kn], GAn = S[S_GA][kn], BAn = S[S_BA][kn];
-                    const f64 fAn = RGBA ? S[S_FA][kn] : 0.0;
-                    const u64 sp = uniform_u64(spv);
-#pragma unroll
-                    for (int r = 0; r < RPW; ++r) {
-                        if (span_lane(sp, r)) {
-                            cr[r] = cr[r] * om + RA;
-                            cg[r] = cg[r] * om + GA;
-                            cb[r] = cb[r] * om + BA;
-                            if (RGBA) ca[r] = fA;
-                        }
-                    }
-                    if (!hm) break;
-                    spv = spn; om = omn; RA = RAn; GA = GAn; BA = BAn; fA = fAn;
-                }
-            }
-            for (; !NR_BLEND_PIPE && hm; hm &= hm - 1) {
+            // registers are updated in place), only the triangles touching
+            // this wave's block
+            for (; hm; hm &= hm - 1) {
                 const int k = (int)__builtin_ctzll(hm);
                 const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
                 const f64 fA = RGBA ? S[S_FA][k] : 0.0;
                 u64 lm[RPW];
-                if (NR_LANE_MASKS) {   // the 4 rows' lane masks, formed by the span phase
-                    const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
-                    const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
-                    lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
-                    lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
-                } else {
-                    const u64 sp = uniform_u64(SP[k][wave]);
-#pragma unroll
-                    for (int r = 0; r < RPW; ++r) lm[r] = span_lanes((u32)(sp >> (16 * r)) & 0xFFFFu);
-                }
+                const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
+                const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
+                lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
+                lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
                     if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
@@ -391,21 +386,27 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             __syncthreads();
             continue;
         }
-        const f64 X = (f64)(x0 + lane);
+        const f64 X = (f64)px;
         for (; hm; hm &= hm - 1) {
             const int k = (int)__builtin_ctzll(hm);
-            const u64 sp = uniform_u64(SP[k][wave]);
+            u64 lm[RPW];
+            {
+                const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
+                const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
+                lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
+                lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
+            }
             // (uniform: read into scalar registers, so the branches below are scalar)
             const bool ztest = DEPTH && !__builtin_amdgcn_readfirstlane((int)ZPASS[k]);   // the depth expression is needed
             if (!GOURAUD && !ztest) {
                 // flat colour, no per-pixel depth: ApplyPixel from the
-                // per-triangle terms on the covered lanes of each row
+                // per-triangle terms on the covered lanes of each step
                 const f64 fA = __longlong_as_double((long long)uniform_u64((u64)__double_as_longlong(S[S_FA][k])));
                 if (fA != 1) {
                     const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        if (span_lane(sp, r)) {
+                        if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
                             cr[r] = cr[r] * om + RA;
                             cg[r] = cg[r] * om + GA;
                             cb[r] = cb[r] * om + BA;
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     const f64 fR = S[S_FR][k], fG = S[S_FG][k], fB = S[S_FB][k];
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        if (span_lane(sp, r)) {
+                        if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
                             cr[r] = fR; cg[r] = fG; cb[r] = fB;
                             if (RGBA) ca[r] = fA;
                         }
@@ -441,11 +442,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             }
 #pragma unroll
             for (int r = 0; r < RPW; ++r) {
-                const int row = wave * RPW + r;
-                if (!span_lane(sp, r)) continue;
+                if (!__builtin_amdgcn_inverse_ballot_w64(lm[r])) continue;
                 f64 w1 = 0, w2 = 0;
                 if (ztest || GOURAUD) {
-                    const f64 dy = (f64)(y0 + row) - sy0;
+                    const f64 dy = (f64)(y0 + lrow0 + r * SR) - sy0;
                     w1 = (pa - e2x * dy) * inv;
                     w2 = (e1x * dy - pb) * inv;
                 }
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // ---- write the tile back once
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-        const i64 py = y0 + wave * RPW + r;
+        const i64 py = y0 + lrow0 + r * SR;
         if (px < fp.W && py < fp.H) {
             f64* p = fp.fb + (py * fp.W + px) * ipp;
             p[0] = cr[r]; p[1] = cg[r]; p[2] = cb[r];

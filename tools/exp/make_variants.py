@@ -72,19 +72,21 @@ PATCHES = {
         ("        if (!sLast) continue;\n",
          "        if (tid == 0) exp_mid |= (__builtin_amdgcn_s_memrealtime() - exp_t0) << 32;\n        if (!sLast) continue;\n"),
     ],
-    "EXP_SHT": [   # shading phase durations summed over all shade_tile calls -> g_acc
-        ("    for (int i = tid; i < HTS; i += NT) ht[i] = 0;\n",
-         "    const u64 sh_t0 = __builtin_amdgcn_s_memrealtime();\n    for (int i = tid; i < HTS; i += NT) ht[i] = 0;\n"),
+    "EXP_SHT": [   # shading phase durations summed over all shade_tile calls -> g_acc (0 hash, 1 records, 2 pixels, 5 overflow pixels)
+        ("    for (int i = tid; i < HS; i += NT) ht[i] = 0;\n",
+         "    const u64 sh_t0 = __builtin_amdgcn_s_memrealtime();\n    for (int i = tid; i < HS; i += NT) ht[i] = 0;\n"),
         ("    __syncthreads();   // every key read: the records may overwrite them\n",
          "    __syncthreads();   // every key read: the records may overwrite them\n    const u64 sh_t1 = __builtin_amdgcn_s_memrealtime();\n"),
-        ("    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    __syncthreads();\n",
-         "    for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    __syncthreads();\n"
+        ("        for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    }\n    __syncthreads();\n",
+         "        for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);\n    }\n    __syncthreads();\n"
          "    const u64 sh_t2 = __builtin_amdgcn_s_memrealtime();\n"),
-        ("        store_colour(fp, gp, px, py, cr, cg, cb, ca);\n    }\n}",
-         "        store_colour(fp, gp, px, py, cr, cg, cb, ca);\n    }\n    __syncthreads();\n"
-         "    if (tid == 0) { const u64 sh_t3 = __builtin_amdgcn_s_memrealtime();\n"
+        ("        store_colour(fp, gp, px, py, cr, cg, cb, ca);\n    }\n    // pass 3b",
+         "        store_colour(fp, gp, px, py, cr, cg, cb, ca);\n    }\n    __syncthreads();\n    const u64 sh_t3 = __builtin_amdgcn_s_memrealtime();\n    // pass 3b"),
+        ("                store_colour(fp, gp, px, py, cr, cg, cb, ca);\n            }\n        }\n    }\n}\n",
+         "                store_colour(fp, gp, px, py, cr, cg, cb, ca);\n            }\n        }\n    }\n    __syncthreads();\n"
+         "    if (tid == 0) { const u64 sh_t4 = __builtin_amdgcn_s_memrealtime();\n"
          "        atomicAdd(&g_acc[0], sh_t1 - sh_t0); atomicAdd(&g_acc[1], sh_t2 - sh_t1); atomicAdd(&g_acc[2], sh_t3 - sh_t2);\n"
-         "        atomicAdd(&g_acc[3], 1ull); atomicAdd(&g_acc[4], (u64)nU); }\n}"),
+         "        atomicAdd(&g_acc[5], sh_t4 - sh_t3); atomicAdd(&g_acc[3], 1ull); atomicAdd(&g_acc[4], (u64)nU); }\n}\n"),
     ],
     "EXP_NOROWS": [
         ("            if (r0 >= r1) continue;\n",

@@ -15,5 +15,5 @@ ctx.flush(); lib.ExpResetAcc()
 for _ in range(5): frame()
 ctx.flush(); lib.ExpGetAcc(out.ctypes.data_as(ctypes.c_void_p))
 n = max(1, int(out[3]))
-print("shade_tile calls %d  winners/tile %.1f  hash %.2f us  records %.2f us  pixels %.2f us" % (
-    n, out[4] / n, out[0] / n / 100, out[1] / n / 100, out[2] / n / 100))
+print("shade_tile calls %d  winners/tile %.1f  hash %.2f us  records %.2f us  pixels %.2f us  overflow pixels %.2f us" % (
+    n, out[4] / n, out[0] / n / 100, out[1] / n / 100, out[2] / n / 100, out[5] / n / 100))

@@ -103,6 +103,8 @@ def main():
                     if k < prow[p]:
                         ms = max(ms, steps[brk[p] + k])
                 it += SPAN + PIX * ms
+                tot["rowsteps"] = tot.get("rowsteps", 0) + 1
+                tot["pixsteps"] = tot.get("pixsteps", 0) + ms
             tot["nested"] += it
             tot["flat"] += (SPAN + PIX) * psteps_flat[c0:c1].max()
             fr = span_s[brk[c0]:brk[c1]].sum()
