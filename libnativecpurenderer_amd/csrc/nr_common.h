@@ -53,8 +53,8 @@ struct TriScratch {
         u64* frect = nullptr; size_t frect_cap = 0;   // per-triangle tile rectangle (count -> emit)
         u32* flist = nullptr; size_t flist_cap = 0;
         u32* dplan = nullptr;
-        u32* h_plan = nullptr;              // pinned, device-mapped copy of the plan totals
-        u32* d_hplan = nullptr;             // its device address
+        u64* h_plan = nullptr;              // pinned, device-mapped copy of the plan totals, (seq << 32) | value
+        u64* d_hplan = nullptr;             // its device address
         hipEvent_t evBin = nullptr;         // binning done (binning stream)
         hipEvent_t evVis = nullptr;         // k_vis done reading the set (main stream)
         bool visRecorded = false;

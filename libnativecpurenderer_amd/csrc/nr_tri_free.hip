@@ -195,7 +195,7 @@ __device__ __forceinline__ int size_class(u32 c, u32 lim) {
 __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
                                                       u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
-                                                      u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
+                                                      u64* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
                                                       u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
     __shared__ u32 sh[3][PLAN_W];
     __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
@@ -275,13 +275,17 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     }
     if (tid == 0) {
         off[ntiles] = ta;
-        const u32 t[4] = {ta, tb, tm, fits ? 1u : 0u};
-        for (int k = 0; k < 4; ++k) {
-            totals[k] = t[k];
-            __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const u32 t[6] = {ta, tb, tm, fits ? 1u : 0u, seq, th};
+        for (int k = 0; k < 4; ++k) totals[k] = t[k];
+        // the host copy (nr_settle polls it): every word carries the batch's
+        // sequence number in its high half and is stored on its own (8-byte
+        // stores are single-copy atomic), so the host needs no ordering between
+        // them and the kernel no release -- a system-scope release writes back
+        // the whole L2 (buffer_wbl2), the dirty frame lines of the raster
+        // running beside this kernel included (C3 -1.2 %, 8-way share -2 %,
+        // profiles/r03_c3/ab_plan_release.txt)
+        for (int k = 0; k < 6; ++k)
+            __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -294,7 +298,7 @@ constexpr int PS_T = 256, PS_W = PS_T / 64, PS = 16;
 __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
                                                       u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                       u32* __restrict__ cur, u32* __restrict__ totals,
-                                                      u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
+                                                      u64* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
                                                       u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
     __shared__ u32 sh[3][PS_W];
     __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
@@ -389,14 +393,10 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
     }
     if (tid == 0) {
         off[ntiles] = ta;
-        const u32 t[4] = {ta, tb, tm, fits ? 1u : 0u};
-        for (int k = 0; k < 4; ++k) {
-            totals[k] = t[k];
-            __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // the batch's sequence number last: the host polls it (nr_settle)
-        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const u32 t[6] = {ta, tb, tm, fits ? 1u : 0u, seq, th};
+        for (int k = 0; k < 4; ++k) totals[k] = t[k];
+        for (int k = 0; k < 6; ++k)   // (host copy: see k_free_plan)
+            __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -417,7 +417,7 @@ template <int T, int PR>
 __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
                                                    u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                    u32* __restrict__ cur, u32* __restrict__ totals,
-                                                   u32* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
+                                                   u64* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
                                                    u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
     constexpr int NWV = T / 64;
     __shared__ u32 sh[4][NWV];
@@ -536,13 +536,10 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     }
     if (tid == 0) {
         off[ntiles] = ta;   // (the same value as the padding stores write there)
-        const u32 t[4] = {ta, tb, tm, fits ? 1u : 0u};
-        for (int k = 0; k < 4; ++k) {
-            totals[k] = t[k];
-            __hip_atomic_store(&host_totals[k], t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __hip_atomic_store(&host_totals[5], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&host_totals[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const u32 t[6] = {ta, tb, tm, fits ? 1u : 0u, seq, th};
+        for (int k = 0; k < 4; ++k) totals[k] = t[k];
+        for (int k = 0; k < 6; ++k)   // (host copy: see k_free_plan)
+            __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1548,6 +1545,16 @@ static hipEvent_t sync_event() {
 // stream -- after the raster that last read set `si`, not after everything
 // queued before on the main stream -- so that it overlaps the previous
 // batch's k_vis (only for immutable inputs: a TriangleBuffer).
+// Host view of a plan kernel's totals (k_free_plan*): word k = (seq << 32) | value, each
+// stored by the device on its own; a batch's totals are complete once every word carries
+// its sequence number.
+static bool plan_ready(const TriScratch::FreeSet& F, u32 seq) {
+    for (int k = 0; k < 6; ++k)
+        if ((u32)(__atomic_load_n(&F.h_plan[k], __ATOMIC_ACQUIRE) >> 32) != seq) return false;
+    return true;
+}
+static u32 plan_val(const TriScratch::FreeSet& F, int k) { return (u32)__atomic_load_n(&F.h_plan[k], __ATOMIC_ACQUIRE); }
+
 static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
                          bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0,
                          u32 knownItems = 0, bool idle = false, u32 knownSplit = 0) {
@@ -1583,8 +1590,8 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     if (sc.fdone_cap != olddone) NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.fdone_cap * sizeof(u32), sa));
     if (!F.dplan) NR_CHECK(hipMalloc(&F.dplan, 4 * sizeof(u32)));
     if (!F.h_plan) {
-        NR_CHECK(hipHostMalloc((void**)&F.h_plan, 8 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
-        F.h_plan[4] = 0;
+        NR_CHECK(hipHostMalloc((void**)&F.h_plan, 8 * sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent));
+        for (int k = 0; k < 8; ++k) F.h_plan[k] = 0;
         NR_CHECK(hipHostGetDevicePointer((void**)&F.d_hplan, F.h_plan, 0));
     }
     // key slots of split tiles' slices (TH * TW keys each): sized from the
@@ -1705,14 +1712,14 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         // exact: read the totals back; if the list or the items did not fit,
         // grow both and bin again (the plan kernel re-zeroed the counters)
         NR_CHECK(hipStreamSynchronize(sb));
-        sc.lastPairs = F.h_plan[0];
-        sc.lastHeavy = F.h_plan[5];
-        sc.lastItems = F.h_plan[1];
-        sc.lastSplit = F.h_plan[2];
+        sc.lastPairs = plan_val(F, 0);
+        sc.lastHeavy = plan_val(F, 5);
+        sc.lastItems = plan_val(F, 1);
+        sc.lastSplit = plan_val(F, 2);
         sc.lastN = (u64)src.n;
-        grid = F.h_plan[1];
-        if (F.h_plan[3]) break;
-        if (attempt > 0 || !grow_list(F.h_plan[0]) || !grow_items(F.h_plan[1]) || !grow_kslot(F.h_plan[2])) {
+        grid = plan_val(F, 1);
+        if (plan_val(F, 3)) break;
+        if (attempt > 0 || !grow_list(plan_val(F, 0)) || !grow_items(plan_val(F, 1)) || !grow_kslot(plan_val(F, 2))) {
             nr_set_error_msg("triangle binning: pair list allocation failed");
             return false;
         }
@@ -1840,16 +1847,16 @@ void settle(RenderContext* ctx) {
     ctx->pendingBatch = nullptr;
     TriScratch& sc = ctx->tri;
     TriScratch::FreeSet& F = sc.fset[pb->set];
-    // wait for the batch's plan (usually long finished): it writes its
-    // sequence number into pinned host memory after the totals -- polling it
-    // avoids an event record per batch (each costs a multi-microsecond
-    // bubble on the stream)
+    // wait for the batch's plan (usually long finished): it writes its totals
+    // into pinned host memory, each word tagged with the batch's sequence
+    // number -- polling them avoids an event record per batch (each costs a
+    // multi-microsecond bubble on the stream)
     const u32 want = pb->seq;
-    for (u64 spin = 0; __atomic_load_n(&F.h_plan[4], __ATOMIC_ACQUIRE) != want; ++spin) {
+    for (u64 spin = 0; !plan_ready(F, want); ++spin) {
         if ((spin & 1023) == 1023) {
             const bool idle = hipStreamQuery(ctx->stream) != hipErrorNotReady &&
                               hipStreamQuery(nr_bin_stream_for(ctx->device)) != hipErrorNotReady;
-            if (idle && __atomic_load_n(&F.h_plan[4], __ATOMIC_ACQUIRE) != want) {
+            if (idle && !plan_ready(F, want)) {
                 nr_set_error_msg("triangle batch: plan result missing (stream idle or failed)");
                 delete pb;
                 return;
@@ -1858,12 +1865,12 @@ void settle(RenderContext* ctx) {
         }
     }
     sc.lastN = (u64)pb->src.n;
-    sc.lastPairs = F.h_plan[0];
-    sc.lastHeavy = F.h_plan[5];
-    sc.lastItems = F.h_plan[1];
-    sc.lastSplit = F.h_plan[2];
-    record_known(pb->tb, pb->key, F.h_plan[0], F.h_plan[5], F.h_plan[1], F.h_plan[2]);   // exact totals, fitted or not
-    if (!F.h_plan[3]) {
+    sc.lastPairs = plan_val(F, 0);
+    sc.lastHeavy = plan_val(F, 5);
+    sc.lastItems = plan_val(F, 1);
+    sc.lastSplit = plan_val(F, 2);
+    record_known(pb->tb, pb->key, plan_val(F, 0), plan_val(F, 5), plan_val(F, 1), plan_val(F, 2));   // exact totals, fitted or not
+    if (!plan_val(F, 3)) {
         // overflow: the batch's later kernels did nothing; re-run it exactly
         // on the main stream, after everything queued so far
         NR_CHECK(hipEventSynchronize(F.evVis));
