@@ -353,6 +353,30 @@ struct FrameParams {
     int frameYUV;
 };
 
+// Frame output of pixel p = (px, py) from its framebuffer value, written by
+// the rasters' own write-back when they cover every owned pixel (a pending
+// clear): the u8 image (cpp:52-57) or, with fp.frameYUV, its YUV420P planes --
+// Y of every pixel, U and V from the even pixel of each 2x2 block (tiles have
+// even sizes and origins, so a block never straddles two).
+__device__ __forceinline__ void store_frame_out(const FrameParams& fp, i64 p, i64 px, i64 py, f64 cr, f64 cg, f64 cb,
+                                                f64 ca) {
+    if (!fp.frameU8) return;
+    const int r8 = nr_to_u8(cr), g8 = nr_to_u8(cg), b8 = nr_to_u8(cb);
+    if (fp.frameYUV) {
+        fp.frameU8[p] = nr_y_of(r8, g8, b8);
+        if (!((px | py) & 1)) {
+            const i64 cw = fp.W >> 1;
+            iu8* up = fp.frameU8 + fp.W * fp.H + (py >> 1) * cw + (px >> 1);
+            up[0] = nr_u_of(r8, g8, b8);
+            up[cw * (fp.H >> 1)] = nr_v_of(r8, g8, b8);
+        }
+    } else {
+        iu8* d8 = fp.frameU8 + p * fp.ipp;
+        d8[0] = (iu8)r8; d8[1] = (iu8)g8; d8[2] = (iu8)b8;
+        if (fp.ipp == 4) d8[3] = nr_to_u8(ca);
+    }
+}
+
 enum Opacity { OPQ_UNKNOWN = 0, OPQ_OPAQUE, OPQ_BLENDED };
 
 template <typename T, size_t K>

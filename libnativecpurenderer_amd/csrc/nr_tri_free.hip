@@ -558,7 +558,7 @@ static bool plan_reg() {
 // the 1024-thread one otherwise: a short k_vis leaves the plan mostly alone and
 // the wider workgroup is faster (C3 8-way share 0.0535 -> 0.0516 ms; C2, 10k
 // triangles, 0.0802 -> 0.069 ms).  NR_PLAN_SMALL=0/1 forces one (A/B).
-static bool plan_small(int period, u64 mask, i64 ntri) {
+static bool owned_share_large(int period, u64 mask, i64 ntri) {
     static const int v = [] {
         const char* e = getenv("NR_PLAN_SMALL");
         return e ? atoi(e) : -1;
@@ -692,32 +692,15 @@ __device__ __forceinline__ void store_depth(const FrameParams& fp, i64 p, u64 kv
     else if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
 }
 
-// Framebuffer (+ frame output) value of pixel p = (px, py), written once.
-// The frame output is the u8 image (cpp:52-57) or, with fp.frameYUV, its
-// YUV420P planes: Y of every pixel, U and V from the even pixel of each 2x2
-// block (tiles have even sizes and origins, so a block never straddles two).
+// Framebuffer (+ frame output, nr_tri.h store_frame_out) value of pixel p =
+// (px, py), written once.
 __device__ __forceinline__ void store_colour(const FrameParams& fp, i64 p, i64 px, i64 py, f64 cr, f64 cg, f64 cb,
                                              f64 ca) {
     const int ipp = fp.ipp;
     f64* dst = fp.fb + p * ipp;
     dst[0] = cr; dst[1] = cg; dst[2] = cb;
     if (ipp == 4) dst[3] = ca;
-    if (fp.frameU8) {
-        const int r8 = nr_to_u8(cr), g8 = nr_to_u8(cg), b8 = nr_to_u8(cb);
-        if (fp.frameYUV) {
-            fp.frameU8[p] = nr_y_of(r8, g8, b8);
-            if (!((px | py) & 1)) {
-                const i64 cw = fp.W >> 1;
-                iu8* up = fp.frameU8 + fp.W * fp.H + (py >> 1) * cw + (px >> 1);
-                up[0] = nr_u_of(r8, g8, b8);
-                up[cw * (fp.H >> 1)] = nr_v_of(r8, g8, b8);
-            }
-        } else {
-            iu8* d8 = fp.frameU8 + p * ipp;
-            d8[0] = (iu8)r8; d8[1] = (iu8)g8; d8[2] = (iu8)b8;
-            if (ipp == 4) d8[3] = nr_to_u8(ca);
-        }
-    }
+    store_frame_out(fp, p, px, py, cr, cg, cb, ca);
 }
 
 // ApplyPixel (cpp:529-547) of the winner's colour.  ca == 1 except for
@@ -1660,7 +1643,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
         // a large owned share (a long k_vis of the previous batch to run beside)
         // takes the narrow plan kernel; an idle GPU the faster wide one
-        const bool besideRaster = !idle && plan_small(fp.period, fp.mask, src.n);
+        const bool besideRaster = !idle && owned_share_large(fp.period, fp.mask, src.n);
         const u32 icap32 = (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull);
         const u32 kcap32 = (u32)std::min<size_t>(sc.kslot_cap / (TH * TW), 0xFFFFFFF0ull);
         const u32 sat = sc.splitAt ? sc.splitAt : split_at(), dsl = sc.dslice ? sc.dslice : dslice();
@@ -1743,7 +1726,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = ext_stop() && !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
-        const bool largeShare = plan_small(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
+        const bool largeShare = owned_share_large(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
         if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<1, false>(fp, sc, F, grid, sa, st, largeShare); }
         else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<2, false>(fp, sc, F, grid, sa, st, largeShare); }
         else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<0, false>(fp, sc, F, grid, sa, st, largeShare); }

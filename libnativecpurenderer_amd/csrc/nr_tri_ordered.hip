@@ -493,6 +493,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             p[0] = cr[r]; p[1] = cg[r]; p[2] = cb[r];
             if (RGBA) p[3] = ca[r];
             if (DEPTH && (fp.depthWrite || fp.pendDepth)) fp.depth[py * fp.W + px] = cz[r];
+            store_frame_out(fp, py * fp.W + px, px, py, cr[r], cg[r], cb[r], RGBA ? ca[r] : 1.0);
         }
     }
     if (COUNT) {
@@ -525,6 +526,12 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
     hipStream_t s = ctx->stream;
     TriScratch& sc = ctx->tri;
     FrameParams fp = frame_params(ctx, src);
+    // with a pending clear every owned tile is rasterised and written back,
+    // so the write-back also produces the frame output (as k_vis does)
+    if (ctx->frameOutput && fp.pendColor) {
+        const size_t n = (size_t)nr_frame_bytes(ctx);
+        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
+    }
     const int ntiles = fp.tiles_x * fp.tiles_y;
 
     BinParams bp;

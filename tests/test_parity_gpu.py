@@ -497,17 +497,26 @@ def test_fused_frame_output_matches_conversion(gpu, fmt, alpha):
     """After the first GatherFrameU8 the resolve writes the frame output
     itself (u8 image, or its YUV420P planes); it must equal GetBufferAsUInt8
     (resp. the YUV420P restatement of it) every frame, including frames with a
-    second (non-clearing) batch, a primitive drawn after the triangles, or a
-    blended batch (ordered raster: converted after it)."""
+    second (non-clearing) batch, a primitive drawn after the triangles, a
+    blended batch after an opaque one (ordered raster: converted after it), or
+    a blended batch right after the clear (the ordered raster's write-back
+    produces the frame output itself)."""
     W, H = 300, 200
     xy, z, c = scenes.triangle_soup(2000, W, H, 15, seed=51, gouraud=True)
+    bxy, bz, bc = scenes.triangle_soup(600, W, H, 40, seed=52, gouraud=False, alpha=(0.2, 0.8))
     ctx = gpu.context(W, H, alpha)
     ctx.set_frame_format(fmt)
     conv = (lambda a: a) if fmt == "rgb" else scenes.yuv420p
-    for frame in range(5):
+    for frame in range(7):
         ctx.set_color(0.05 * frame, 0.05 * frame, 0.05 * frame, 0.05 * frame)
         ctx.set_depth_state(True, True)
         ctx.clear_depth()
+        if frame >= 5:   # ordered raster with the pending clear (Z test off / on without write)
+            ctx.set_depth_state(frame == 6, False)
+            ctx.draw_triangles(bxy, bc, z=bz, gouraud=False)
+            ctx.gather_frame_u8()
+            assert np.array_equal(ctx.get_frame_u8(), conv(ctx.get_buffer_as_uint8_numpy())), frame
+            continue
         ctx.draw_triangles(xy, c, z=z)
         if frame == 2:
             ctx.draw_triangles(xy[:100] + 7.0, c[:100], z=z[:100] * 0.5)

@@ -1,4 +1,4 @@
-# Round 3 session J: GPU suite at the working tree (tagged plan totals), the default bench line (with extras),
+# Round 3 session J/M: GPU suite at the working tree, the default bench line (with extras),
 # then the C3 profile (kernel trace + PMC passes) and the per-config HBM traffic of C3 and C5.
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 > gpurun_out/pytest_gpu.log 2>&1
