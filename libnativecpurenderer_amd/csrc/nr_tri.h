@@ -377,6 +377,57 @@ __device__ __forceinline__ void store_frame_out(const FrameParams& fp, i64 p, i6
     }
 }
 
+// Per-triangle setup record of the ordered raster, formed once per triangle
+// by the counting kernel (k_tri_count, or k_free_count for a binned ordered batch) (a triangle of C5 lies in ~100 tiles; the raster used to set
+// it up again in each): screen vertices, edge slopes, 1/den, depths and the
+// depth-pass bound (zpass_bound).  16 doubles, 128 B, 16-B aligned.
+enum { R_X0 = 0, R_Y0, R_X1, R_Y1, R_X2, R_Y2, R_SL0, R_SL1, R_SL2, R_INV, R_Z0, R_Z1, R_Z2, R_FLAGS, ORec = 16 };
+
+// Depth-pass proof (zpass_all): with the Z test on and Z write off, a
+// triangle passes the LESS test on every pixel the exact span rule covers when
+// all of them quantise (nr_quantize_depth) strictly below the tile's smallest
+// depth zmin.  For a triangle with G = max|edge| / |den|, bbox extent S and
+// coordinate magnitude M, G*S <= 1e4 and G*M <= 1e4 bound the computed
+// barycentrics of covered pixels to [-1e-10, 1 + 1e-10] (span-rule crossings
+// and the w1/w2 expressions both err by O(u (G S + G M)), u = 2^-53; den's
+// cancellation by O(u G S) relative), so with |z| <= 2 the computed depth is at
+// most max(z) + 1e-9 (< max(z) + 1e-8, the bound used).  The triangle-only
+// part is this bound, quantised, or 0xFFFFFFFF when the analysis does not
+// apply (no tile minimum lies above it): zpass_all == (zpass_bound < zmin).
+__device__ __forceinline__ u32 zpass_bound(const f64 (&sx)[3], const f64 (&sy)[3], f64 e1x, f64 e1y, f64 e2x, f64 e2y,
+                                           f64 den, f64 z0, f64 z1, f64 z2) {
+    if (!tri_finite(sx, sy) || den == 0) return 0xFFFFFFFFu;
+    if (!(fabs(z0) <= 2 && fabs(z1) <= 2 && fabs(z2) <= 2)) return 0xFFFFFFFFu;   // (NaN: no bound)
+    const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
+    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
+    const f64 e = fmax(fmax(fabs(e1x), fabs(e1y)), fmax(fabs(e2x), fabs(e2y)));
+    const f64 G = e / fabs(den);
+    const f64 S = (xmx - xmn) + (ymx - ymn) + 4.0;
+    const f64 M = fmax(fmax(fabs(xmn), fabs(xmx)), fmax(fabs(ymn), fabs(ymx))) + 1.0;
+    if (!(G * S <= 1e4 && G * M <= 1e4)) return 0xFFFFFFFFu;
+    return nr_quantize_depth(fmax(fmax(z0, z1), z2) + 1e-8);
+}
+
+// Setup record of triangle t (screen vertices sx, sy, valid: finite, den != 0).
+__device__ __forceinline__ void write_ordered_record(f64* rec, i64 t, const f64 (&sx)[3], const f64 (&sy)[3],
+                                                     const f64* zsrc) {
+    const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
+    const f64 den = e1x * e2y - e2x * e1y;
+    f64 sl[3];
+    edge_slopes(sx, sy, sl);
+    f64 z0 = 0, z1 = 0, z2 = 0;
+    if (zsrc) { z0 = zsrc[t * 3]; z1 = zsrc[t * 3 + 1]; z2 = zsrc[t * 3 + 2]; }
+    const u64 flags = 1ull | ((u64)zpass_bound(sx, sy, e1x, e1y, e2x, e2y, den, z0, z1, z2) << 32);
+    double2* r = reinterpret_cast<double2*>(rec + t * ORec);
+    r[0] = make_double2(sx[0], sy[0]);
+    r[1] = make_double2(sx[1], sy[1]);
+    r[2] = make_double2(sx[2], sy[2]);
+    r[3] = make_double2(sl[0], sl[1]);
+    r[4] = make_double2(sl[2], 1.0 / den);
+    r[5] = make_double2(z0, z1);
+    r[6] = make_double2(z2, __longlong_as_double((long long)flags));
+}
+
 enum Opacity { OPQ_UNKNOWN = 0, OPQ_OPAQUE, OPQ_BLENDED };
 
 template <typename T, size_t K>
@@ -402,13 +453,27 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src);
 void finish_batch(RenderContext* ctx, const FrameParams& fp);
 
 // the two rasterisers (host side)
-void draw_ordered(RenderContext* ctx, const TriSrc& src);
+// ordered batches: binned like the order-free ones (count / plan / emit, on the
+// binning stream beside the previous raster) when the frame has at most
+// ORD_BIN_TILES tiles, each tile's list sorted in LDS (k_tile_sort); the
+// global-sort path (draw_ordered_sorted) otherwise, and for a batch with a tile
+// of more than ORD_SORT_CAP triangles (detected by the plan, re-run)
+void draw_ordered(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned);
+void draw_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp);
+constexpr u32 ORD_SORT_CAP = 8192;    // longest tile list the ordered raster sorts in LDS
+constexpr int ORD_BIN_TILES = 16384;  // tiles of the binned ordered path (the register plan kernel's limit)
+// binned ordered batches: k_tile_sort sorts each tile's list [off[t], off[t + 1])
+// in place (binning stream), then the raster runs one workgroup per tile; both
+// are no-ops unless plan[3] (fits)
+void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, hipStream_t s, hipEvent_t stop);
+void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* off, const u32* plan, const f64* rec,
+                           int ntiles, hipStream_t s, hipEvent_t stop);
 // tb: the batch is that (immutable) TriangleBuffer, so its binning may overlap
 // the previous raster and a repeat draw is sized from its known totals;
 // callerOwned: the arrays are the caller's device memory (DrawTrianglesDevice),
 // so the batch is sized exactly in the call -- an overflow re-run never reads
 // them after it returns
-void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned);
+void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned, bool ordered = false);
 void settle(RenderContext* ctx);
 
 }  // namespace nrtri

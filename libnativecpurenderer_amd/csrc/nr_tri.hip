@@ -125,7 +125,7 @@ void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 
     const bool freeEligible = ctx->ct[3] == 1 && ctx->forceOrdered == 0;
     if (freeEligible && opq == OPQ_UNKNOWN) opq = device_opacity(ctx, src);
     if (freeEligible && opq == OPQ_OPAQUE) draw_free(ctx, src, tb, callerOwned);
-    else draw_ordered(ctx, src);
+    else draw_ordered(ctx, src, tb, callerOwned);
 }
 
 }  // namespace

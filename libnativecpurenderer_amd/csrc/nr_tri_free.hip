@@ -69,9 +69,11 @@ __device__ __forceinline__ u64 pack_rect(int tx0, int tx1, int ty0, int ty1) {
     return (u64)(u32)tx0 | ((u64)(u32)tx1 << 16) | ((u64)(u32)ty0 << 32) | ((u64)(u32)ty1 << 48);
 }
 
-template <bool LDSH>
+// REC (ordered batches): also the triangle's setup record for the ordered
+// raster (write_ordered_record), formed once here instead of in every tile.
+template <bool LDSH, bool REC = false>
 __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __restrict__ tile_cnt, int ntiles,
-                                                    u64* __restrict__ rects) {
+                                                    u64* __restrict__ rects, f64* __restrict__ rec = nullptr) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
     const i64 base = (i64)blockIdx.x * 256 * TPT;
@@ -100,6 +102,7 @@ __global__ __launch_bounds__(256) void k_free_count(const BinParams bp, u32* __r
         const bool hit = tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1);
         rects[t] = hit ? pack_rect(tx0, tx1, ty0, ty1) : NO_RECT;
         if (!hit) continue;
+        if (REC) write_ordered_record(rec, t, sx, sy, bp.src.z);   // (hit: finite, den != 0)
         for (int ty = ty0; ty <= ty1; ++ty) {
             if (!owned_row(ty, bp.period, bp.mask)) continue;
             const int hrow = (LDSH ? owned_ord(bp, ty) : ty) * bp.tiles_x;
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     }
     if (tid == 0) {
         off[ntiles] = ta;
-        const u32 t[6] = {ta, tb, tm, fits ? 1u : 0u, seq, th};
+        const u32 t[7] = {ta, tb, tm, fits ? 1u : 0u, seq, th, 0u};
         for (int k = 0; k < 4; ++k) totals[k] = t[k];
         // the host copy (nr_settle polls it): every word carries the batch's
         // sequence number in its high half and is stored on its own (8-byte
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         // the whole L2 (buffer_wbl2), the dirty frame lines of the raster
         // running beside this kernel included (C3 -1.2 %, 8-way share -2 %,
         // profiles/r03_c3/ab_plan_release.txt)
-        for (int k = 0; k < 6; ++k)
+        for (int k = 0; k < 7; ++k)
             __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -393,9 +396,9 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
     }
     if (tid == 0) {
         off[ntiles] = ta;
-        const u32 t[6] = {ta, tb, tm, fits ? 1u : 0u, seq, th};
+        const u32 t[7] = {ta, tb, tm, fits ? 1u : 0u, seq, th, 0u};
         for (int k = 0; k < 4; ++k) totals[k] = t[k];
-        for (int k = 0; k < 6; ++k)   // (host copy: see k_free_plan)
+        for (int k = 0; k < 7; ++k)   // (host copy: see k_free_plan)
             __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -418,9 +421,10 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
                                                    u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
                                                    u32* __restrict__ cur, u32* __restrict__ totals,
                                                    u64* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
-                                                   u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
+                                                   u32 slice_target, u32 kcap, u32 split_at, u32 dslice, u32 maxc) {
     constexpr int NWV = T / 64;
     __shared__ u32 sh[4][NWV];
+    __shared__ u32 smax;   // longest tile list (ordered batches sort each list in LDS: <= maxc, 0 = no limit)
     __shared__ u32 csh[PLAN_NB][NWV];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int per = (((ntiles + T - 1) / T) + 3) & ~3;
@@ -432,12 +436,16 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
         if (4 * q < per) v = reinterpret_cast<const uint4*>(cnt + i0)[q];
         c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
     }
-    u32 a = 0, hv = 0;
+    u32 a = 0, hv = 0, mx = 0;
 #pragma unroll
     for (int j = 0; j < PR; ++j) {
         a += c[j];
         hv += c[j] >= HEAVY_PAIRS ? 1u : 0u;
+        mx = c[j] > mx ? c[j] : mx;
     }
+    if (tid == 0) smax = 0;
+    __syncthreads();
+    if (maxc) atomicMax(&smax, mx);
     const u32 ia = wave_scan(a, lane), ih = wave_scan(hv, lane);
     if (lane == 63) { sh[0][w] = ia; sh[1][w] = ih; }
     __syncthreads();
@@ -483,7 +491,7 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     u32 tb = 0, tm = 0;
 #pragma unroll
     for (int k = 0; k < NWV; ++k) { tb += sh[2][k]; tm += sh[3][k]; }
-    const bool fits = ta <= cap && tb <= icap && tm <= kcap;
+    const bool fits = ta <= cap && tb <= icap && tm <= kcap && (!maxc || smax <= maxc);
     // class ranges, largest class first, and each wave's base inside them:
     // thread k < PLAN_NB turns column k of csh into the wave bases of class k.
     // Every column is read (into registers) before any is rewritten: thread k
@@ -536,9 +544,9 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     }
     if (tid == 0) {
         off[ntiles] = ta;   // (the same value as the padding stores write there)
-        const u32 t[6] = {ta, tb, tm, fits ? 1u : 0u, seq, th};
+        const u32 t[7] = {ta, tb, tm, fits ? 1u : 0u, seq, th, smax};
         for (int k = 0; k < 4; ++k) totals[k] = t[k];
-        for (int k = 0; k < 6; ++k)   // (host copy: see k_free_plan)
+        for (int k = 0; k < 7; ++k)   // (host copy: see k_free_plan)
             __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -1451,6 +1459,7 @@ struct PendingBatch {
     u32 seq;
     TriangleBuffer* tb;   // non-null: record the validated totals as its known sizes
     BinKey key;
+    bool ordered;         // rasterised by the ordered raster (binned)
 };
 
 static BinKey bin_key(const BinParams& bp) {
@@ -1532,15 +1541,19 @@ static hipEvent_t sync_event() {
 // stored by the device on its own; a batch's totals are complete once every word carries
 // its sequence number.
 static bool plan_ready(const TriScratch::FreeSet& F, u32 seq) {
-    for (int k = 0; k < 6; ++k)
+    for (int k = 0; k < 7; ++k)
         if ((u32)(__atomic_load_n(&F.h_plan[k], __ATOMIC_ACQUIRE) >> 32) != seq) return false;
     return true;
 }
 static u32 plan_val(const TriScratch::FreeSet& F, int k) { return (u32)__atomic_load_n(&F.h_plan[k], __ATOMIC_ACQUIRE); }
 
-static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
-                         bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0,
-                         u32 knownItems = 0, bool idle = false, u32 knownSplit = 0) {
+// Returns ENQ_FAIL, ENQ_OK, or (exact, ordered) ENQ_SORTED: a tile list is
+// longer than the ordered raster sorts in LDS -- nothing was rasterised; the
+// caller takes the global-sort path.
+enum { ENQ_FAIL = 0, ENQ_OK = 1, ENQ_SORTED = 2 };
+static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp,
+                        bool exact, int si, bool pipelined, u32* seqOut, u64 knownPairs = 0,
+                        u32 knownItems = 0, bool idle = false, u32 knownSplit = 0, bool ordered = false) {
     hipStream_t sa = ctx->stream;
     hipStream_t sb = pipelined ? nr_bin_stream_for(ctx->device) : sa;
     TriScratch& sc = ctx->tri;
@@ -1560,7 +1573,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     u32* tb[3] = {F.fcnt, F.foff, F.fcur};
     const size_t oldcap = F.ftile_cap;
     // (k_free_plan_r reads and writes the tile arrays as 16-byte vectors up to TILE_ARR)
-    if (!grow_set(tb, &F.ftile_cap, std::max<size_t>((size_t)ntiles + 1, TILE_ARR))) return false;
+    if (!grow_set(tb, &F.ftile_cap, std::max<size_t>((size_t)ntiles + 1, TILE_ARR))) return ENQ_FAIL;
     F.fcnt = tb[0]; F.foff = tb[1]; F.fcur = tb[2];
     if (F.ftile_cap != oldcap) {   // counters start at zero; k_free_plan re-zeroes them after each use
         NR_CHECK(hipMemsetAsync(F.fcnt, 0, F.ftile_cap * sizeof(u32), sb));
@@ -1568,7 +1581,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     }
     u32* db[1] = {sc.fdone};
     const size_t olddone = sc.fdone_cap;
-    if (!grow_set(db, &sc.fdone_cap, (size_t)ntiles + 1)) return false;
+    if (!grow_set(db, &sc.fdone_cap, (size_t)ntiles + 1)) return ENQ_FAIL;
     sc.fdone = db[0];
     if (sc.fdone_cap != olddone) NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.fdone_cap * sizeof(u32), sa));
     if (!F.dplan) NR_CHECK(hipMalloc(&F.dplan, 4 * sizeof(u32)));
@@ -1606,22 +1619,29 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     };
     if (F.frect_cap < (size_t)src.n) quiesce();
     u64* rb[1] = {F.frect};
-    if (!grow_set(rb, &F.frect_cap, (size_t)src.n)) return false;
+    if (!grow_set(rb, &F.frect_cap, (size_t)src.n)) return ENQ_FAIL;
     F.frect = rb[0];
+    if (ordered) {   // the ordered raster's per-triangle setup records
+        const size_t need = (size_t)std::max<i64>(src.n, 1) * ORec;
+        if (F.frec_cap < need) quiesce();
+        f64* rr[1] = {F.frec};
+        if (!grow_set(rr, &F.frec_cap, need)) return ENQ_FAIL;
+        F.frec = rr[0];
+    }
     size_t cap;
     if (!exact) {
         const u64 est = std::max<u64>(std::max<u64>(std::max<u64>(sc.lastPairs + sc.lastPairs / 4, (u64)src.n * 2), 1u << 20),
                                       knownPairs);
         cap = (size_t)std::min<u64>(sc.capOverride ? sc.capOverride : est, 0xFFFFFFF0ull);
-        if (!grow_list(cap)) return false;
+        if (!grow_list(cap)) return ENQ_FAIL;
         if (!sc.capOverride) cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
         // work items: at most one per tile + one per full slice of the list,
         // twice that with dense tiles split into row halves (NR_ROW_SPLIT)
-        if (!grow_items((size_t)ntiles + cap / SLICE_MIN + 2)) return false;
+        if (!grow_items((size_t)ntiles + cap / SLICE_MIN + 2)) return ENQ_FAIL;
         if (!grow_kslot(std::max<size_t>(std::max<size_t>((size_t)sc.lastSplit + sc.lastSplit / 4, knownSplit), 1024)))
-            return false;
+            return ENQ_FAIL;
     } else {
-        if (!grow_list(1) || !grow_items(1) || !grow_kslot(std::max<u32>(sc.lastSplit, 1))) return false;
+        if (!grow_list(1) || !grow_items(1) || !grow_kslot(std::max<u32>(sc.lastSplit, 1))) return ENQ_FAIL;
         cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
     }
 
@@ -1633,8 +1653,14 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     u32 grid;
     for (int attempt = 0;; ++attempt) {
         nr_timing_begin_on(ctx, NRK_TRI_COUNT, &e0, &e1, sb);
-        if (ldsh) hipLaunchKernelGGL(k_free_count<true>, dim3(gb), dim3(256), hbytes, sb, bp, F.fcnt, ntiles, F.frect);
-        else hipLaunchKernelGGL(k_free_count<false>, dim3(gb), dim3(256), 0, sb, bp, F.fcnt, ntiles, F.frect);
+        if (ordered) {
+            if (ldsh) hipLaunchKernelGGL((k_free_count<true, true>), dim3(gb), dim3(256), hbytes, sb, bp, F.fcnt, ntiles, F.frect, F.frec);
+            else hipLaunchKernelGGL((k_free_count<false, true>), dim3(gb), dim3(256), 0, sb, bp, F.fcnt, ntiles, F.frect, F.frec);
+        } else if (ldsh) {
+            hipLaunchKernelGGL((k_free_count<true>), dim3(gb), dim3(256), hbytes, sb, bp, F.fcnt, ntiles, F.frect, nullptr);
+        } else {
+            hipLaunchKernelGGL((k_free_count<false>), dim3(gb), dim3(256), 0, sb, bp, F.fcnt, ntiles, F.frect, nullptr);
+        }
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_COUNT, e0, e1, sb);
 
@@ -1645,9 +1671,11 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         // takes the narrow plan kernel; an idle GPU the faster wide one
         const bool besideRaster = !idle && owned_share_large(fp.period, fp.mask, src.n);
         const u32 icap32 = (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull);
-        const u32 kcap32 = (u32)std::min<size_t>(sc.kslot_cap / (TH * TW), 0xFFFFFFF0ull);
+        // (an ordered batch uses no key slots, and its lists must fit the raster's LDS sort)
+        const u32 kcap32 = ordered ? 0xFFFFFFFFu : (u32)std::min<size_t>(sc.kslot_cap / (TH * TW), 0xFFFFFFF0ull);
+        const u32 maxc = ordered ? ORD_SORT_CAP : 0u;
         const u32 sat = sc.splitAt ? sc.splitAt : split_at(), dsl = sc.dslice ? sc.dslice : dslice();
-        if (plan_reg() && !besideRaster && ntiles <= PLAN_T * PR_MAX) {
+        if ((plan_reg() && !besideRaster && ntiles <= PLAN_T * PR_MAX) || ordered) {   // (ordered: ntiles <= ORD_BIN_TILES)
             // the register plan: one 1024-thread workgroup, PR = tiles per
             // thread -> 4, 8 or 16 (at PR 16 its tile counts, class counters and
             // offsets take ~100 VGPRs; __launch_bounds__(1024) allows 128, so no
@@ -1658,7 +1686,7 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
             const int per = (ntiles + PLAN_T - 1) / PLAN_T;
 #define NR_PLAN_R(PP) hipLaunchKernelGGL((k_free_plan_r<PLAN_T, PP>), dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, \
                                          fp.tiles_x, fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, \
-                                         (u32)cap, icap32, seq, slice_target(), kcap32, sat, dsl)
+                                         (u32)cap, icap32, seq, slice_target(), kcap32, sat, dsl, maxc)
             if (per <= 4) NR_PLAN_R(4); else if (per <= 8) NR_PLAN_R(8); else NR_PLAN_R(16);
 #undef NR_PLAN_R
         }
@@ -1702,9 +1730,10 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
         sc.lastN = (u64)src.n;
         grid = plan_val(F, 1);
         if (plan_val(F, 3)) break;
+        if (ordered && plan_val(F, 6) > ORD_SORT_CAP) return ENQ_SORTED;
         if (attempt > 0 || !grow_list(plan_val(F, 0)) || !grow_items(plan_val(F, 1)) || !grow_kslot(plan_val(F, 2))) {
             nr_set_error_msg("triangle binning: pair list allocation failed");
-            return false;
+            return ENQ_FAIL;
         }
         cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
     }
@@ -1712,17 +1741,31 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
     const bool xs = ext_stop() && sb != sa && !e1;   // no timing events around the kernel
     hipEvent_t binStop = xs ? F.evBin : nullptr;
-    if (ldsh) hipExtLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), (u32)hbytes, sb, nullptr, binStop, 0, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, (const u32*)F.dplan);
-    else hipExtLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, sb, nullptr, binStop, 0, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, (const u32*)F.dplan);
+    hipEvent_t emitStop = ordered ? nullptr : binStop;   // (ordered: the list sort ends the binning)
+    if (ldsh) hipExtLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), (u32)hbytes, sb, nullptr, emitStop, 0, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, (const u32*)F.dplan);
+    else hipExtLaunchKernelGGL(k_free_emit<false>, dim3(gb), dim3(256), 0, sb, nullptr, emitStop, 0, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, (const u32*)F.dplan);
     NR_CHECK(hipGetLastError());
     nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
+    if (ordered) {   // each tile's list into submission order
+        nr_timing_begin_on(ctx, NRK_TRI_SORT, &e0, &e1, sb);
+        launch_tile_sort(F.foff, F.flist, F.dplan, ntiles, sb, binStop);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end_on(ctx, NRK_TRI_SORT, e0, e1, sb);
+    }
     if (sb != sa) {
         if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
         NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
     }
 
     bool visDone = false;
-    if (grid > 0) {
+    if (ordered) {   // one workgroup per tile, its list sorted in LDS
+        nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
+        const bool vs = ext_stop() && !e1;
+        launch_ordered_binned(fp, F.flist, F.foff, F.dplan, F.frec, ntiles, sa, vs ? F.evVis : nullptr);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+        visDone = vs;
+    } else if (grid > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = ext_stop() && !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
@@ -1736,12 +1779,14 @@ static bool free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParam
     }
     if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
     F.visRecorded = true;
-    return true;
+    return ENQ_OK;
 }
 
 }  // namespace
 
-void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned) {
+// ordered: the batch is rasterised by the ordered raster (blending, Z test
+// without write...): the same binning, each tile's list sorted in LDS.
+void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned, bool ordered) {
     FrameParams fp = frame_params(ctx, src);
     if (ctx->frameOutput && fp.pendColor) {
         const size_t n = (size_t)nr_frame_bytes(ctx);
@@ -1774,8 +1819,9 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         const char* e = getenv("NR_KNOWN_SIZES");
         return e ? atoi(e) : 1;
     }();
-    const bool known = knownMode != 0 && (fp.period == 1 || knownMode == 2) && tb && tb->known && !sc.capOverride &&
-                       memcmp(&tb->knownKey, &key, sizeof key) == 0;
+    // (ordered batches are always validated: their plan also checks the list lengths)
+    const bool known = !ordered && knownMode != 0 && (fp.period == 1 || knownMode == 2) && tb && tb->known &&
+                       !sc.capOverride && memcmp(&tb->knownKey, &key, sizeof key) == 0;
     if (known && !exact) {   // this batch's totals pick the k_vis variant (launch_vis)
         sc.lastN = (u64)src.n;
         sc.lastPairs = tb->knownPairs;
@@ -1806,16 +1852,21 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         if (q == hipErrorNotReady) (void)hipGetLastError();   // an answer, not a failure
         else if (q != hipSuccess) NR_CHECK(q);                 // a real asynchronous error: latch it
     }
-    if (!free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact && !idle, &seq,
-                      known ? tb->knownPairs : 0, known ? tb->knownItems : 0, idle, known ? tb->knownSplit : 0))
+    const int r = free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact && !idle, &seq,
+                               known ? tb->knownPairs : 0, known ? tb->knownItems : 0, idle, known ? tb->knownSplit : 0,
+                               ordered);
+    if (r == ENQ_FAIL) return;
+    if (r == ENQ_SORTED) {   // (exact) a tile list too long for the LDS sort
+        draw_ordered_sorted(ctx, src, fp, bp);
         return;
+    }
     if (exact) {
-        record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems, sc.lastSplit);
+        if (!ordered) record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems, sc.lastSplit);
     } else if (!known) {
-        PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq, tb, key};
+        PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq, tb, key, ordered};
         ctx->pendingBatch = pb;
     }
-    ctx->lastPath = 1;
+    ctx->lastPath = ordered ? 2 : 1;
     finish_batch(ctx, fp);
 }
 
@@ -1852,13 +1903,18 @@ void settle(RenderContext* ctx) {
     sc.lastHeavy = plan_val(F, 5);
     sc.lastItems = plan_val(F, 1);
     sc.lastSplit = plan_val(F, 2);
-    record_known(pb->tb, pb->key, plan_val(F, 0), plan_val(F, 5), plan_val(F, 1), plan_val(F, 2));   // exact totals, fitted or not
+    if (!pb->ordered)   // exact totals, fitted or not
+        record_known(pb->tb, pb->key, plan_val(F, 0), plan_val(F, 5), plan_val(F, 1), plan_val(F, 2));
     if (!plan_val(F, 3)) {
-        // overflow: the batch's later kernels did nothing; re-run it exactly
-        // on the main stream, after everything queued so far
+        // overflow (or, ordered, a tile list too long for the LDS sort): the
+        // batch's later kernels did nothing; re-run it exactly on the main
+        // stream, after everything queued so far
         NR_CHECK(hipEventSynchronize(F.evVis));
         u32 seq = 0;
-        free_enqueue(ctx, pb->src, pb->fp, pb->bp, true, pb->set, false, &seq);   // context flags applied at the first launch
+        const bool sorted = pb->ordered && plan_val(F, 6) > ORD_SORT_CAP;
+        if (sorted || free_enqueue(ctx, pb->src, pb->fp, pb->bp, true, pb->set, false, &seq, 0, 0, false, 0, pb->ordered) ==
+                          ENQ_SORTED)
+            draw_ordered_sorted(ctx, pb->src, pb->fp, pb->bp);   // context flags applied at the first launch
     }
     delete pb;
 }

@@ -17,6 +17,7 @@
 //                   written once; a pending uniform clear is applied on chip.
 #include "nr_tri.h"
 
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 namespace nrtri {
@@ -42,37 +43,6 @@ constexpr int SR = 64 / BW;      // rows per step
 constexpr int NQ = TW / BW;      // column windows of the tile
 static_assert(BW * SR == 64 && NQ * (TH / (RPW * SR)) == NWAVE, "wave blocks tile the tile");
 
-// Per-triangle setup record of the ordered raster, formed once per triangle
-// by k_tri_count (a triangle of C5 lies in ~100 tiles; the raster used to set
-// it up again in each): screen vertices, edge slopes, 1/den, depths and the
-// depth-pass bound (zpass_bound).  16 doubles, 128 B, 16-B aligned.
-enum { R_X0 = 0, R_Y0, R_X1, R_Y1, R_X2, R_Y2, R_SL0, R_SL1, R_SL2, R_INV, R_Z0, R_Z1, R_Z2, R_FLAGS, ORec = 16 };
-
-// Depth-pass proof (zpass_all): with the Z test on and Z write off, a
-// triangle passes the LESS test on every pixel the exact span rule covers when
-// all of them quantise (nr_quantize_depth) strictly below the tile's smallest
-// depth zmin.  For a triangle with G = max|edge| / |den|, bbox extent S and
-// coordinate magnitude M, G*S <= 1e4 and G*M <= 1e4 bound the computed
-// barycentrics of covered pixels to [-1e-10, 1 + 1e-10] (span-rule crossings
-// and the w1/w2 expressions both err by O(u (G S + G M)), u = 2^-53; den's
-// cancellation by O(u G S) relative), so with |z| <= 2 the computed depth is at
-// most max(z) + 1e-9 (< max(z) + 1e-8, the bound used).  The triangle-only
-// part is this bound, quantised, or 0xFFFFFFFF when the analysis does not
-// apply (no tile minimum lies above it): zpass_all == (zpass_bound < zmin).
-__device__ __forceinline__ u32 zpass_bound(const f64 (&sx)[3], const f64 (&sy)[3], f64 e1x, f64 e1y, f64 e2x, f64 e2y,
-                                           f64 den, f64 z0, f64 z1, f64 z2) {
-    if (!tri_finite(sx, sy) || den == 0) return 0xFFFFFFFFu;
-    if (!(fabs(z0) <= 2 && fabs(z1) <= 2 && fabs(z2) <= 2)) return 0xFFFFFFFFu;   // (NaN: no bound)
-    const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
-    const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
-    const f64 e = fmax(fmax(fabs(e1x), fabs(e1y)), fmax(fabs(e2x), fabs(e2y)));
-    const f64 G = e / fabs(den);
-    const f64 S = (xmx - xmn) + (ymx - ymn) + 4.0;
-    const f64 M = fmax(fmax(fabs(xmn), fabs(xmx)), fmax(fabs(ymn), fabs(ymx))) + 1.0;
-    if (!(G * S <= 1e4 && G * M <= 1e4)) return 0xFFFFFFFFu;
-    return nr_quantize_depth(fmax(fmax(z0, z1), z2) + 1e-8);
-}
-
 __global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned long long* __restrict__ cnt,
                                                    f64* __restrict__ rec) {
     const i64 t = (i64)blockIdx.x * 256 + threadIdx.x;
@@ -88,22 +58,7 @@ __global__ __launch_bounds__(256) void k_tri_count(const BinParams bp, unsigned 
     }
     cnt[t] = c;
     if (!c) return;   // never listed: no record needed
-    const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-    const f64 den = e1x * e2y - e2x * e1y;
-    f64 sl[3];
-    edge_slopes(sx, sy, sl);
-    f64 z0 = 0, z1 = 0, z2 = 0;
-    if (bp.src.z) { z0 = bp.src.z[t * 3]; z1 = bp.src.z[t * 3 + 1]; z2 = bp.src.z[t * 3 + 2]; }
-    // (tri_tiles lists only finite triangles with den != 0: valid)
-    const u64 flags = 1ull | ((u64)zpass_bound(sx, sy, e1x, e1y, e2x, e2y, den, z0, z1, z2) << 32);
-    double2* r = reinterpret_cast<double2*>(rec + t * ORec);
-    r[0] = make_double2(sx[0], sy[0]);
-    r[1] = make_double2(sx[1], sy[1]);
-    r[2] = make_double2(sx[2], sy[2]);
-    r[3] = make_double2(sl[0], sl[1]);
-    r[4] = make_double2(sl[2], 1.0 / den);
-    r[5] = make_double2(z0, z1);
-    r[6] = make_double2(z2, __longlong_as_double((long long)flags));
+    write_ordered_record(rec, t, sx, sy, bp.src.z);   // (tri_tiles lists only finite triangles with den != 0)
 }
 
 __global__ __launch_bounds__(256) void k_tri_emit(const BinParams bp, const unsigned long long* __restrict__ off,
@@ -170,19 +125,23 @@ __device__ __forceinline__ u64 window_bits(int xs, int xe) {
 
 // RGBA: the context has an alpha channel (ipp 4).  An RGB context never
 // stores alpha, so the per-fragment alpha moves are dropped.
-template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA>
+// BINNED: the tile's list comes from the order-free binning, sorted per tile
+// by k_tile_sort (tstart = the plan's list offsets: [off[tile], off[tile + 1]));
+// the batch is a no-op unless plan[3] (fits); otherwise [tstart, tend) of the
+// globally sorted pairs.
+template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA, bool BINNED>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
                                                     const u32* __restrict__ tstart, const u32* __restrict__ tend,
-                                                    const f64* __restrict__ rec) {
+                                                    const f64* __restrict__ rec, const u32* __restrict__ plan) {
     const int tile = blockIdx.x;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
     const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
     // (wave: uniform, so the per-wave masks and addresses below stay scalar)
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (BINNED && !plan[3]) return;
     if (!owned_row(ty, fp.period, fp.mask)) return;
-    const u32 ls = tstart[tile], le = tend[tile];
+    const u32 ls = tstart[tile], le = BINNED ? tstart[tile + 1] : tend[tile];
     if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
-
     __shared__ f64 S[S_NSLOT][CH];
     // the lane masks of a wave's RPW steps for triangle k (bit l: lane l's
     // pixel of that step is covered), formed by the span phase's 512 threads
@@ -503,43 +462,102 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
 }
 
-template <bool G, bool D, bool C>
-void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s,
-                   const f64* rec) {
-    if (fp.ipp == 4) hipLaunchKernelGGL((k_tile_raster<G, D, C, true>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te, rec);
-    else hipLaunchKernelGGL((k_tile_raster<G, D, C, false>), dim3(ntiles), dim3(WG), 0, s, fp, list, ts, te, rec);
+// Sorts each tile's list of a binned ordered batch into submission order, in
+// place: one workgroup per tile, the list (<= ORD_SORT_CAP entries: the plan
+// guarantees it, or the batch is a no-op) bitonic-sorted in LDS.  It runs on
+// the binning stream after k_free_emit, beside the previous batch's raster.
+constexpr int SORT_T = 512;
+__global__ __launch_bounds__(SORT_T) void k_tile_sort(const u32* __restrict__ off, u32* __restrict__ list,
+                                                      const u32* __restrict__ plan) {
+    if (!plan[3]) return;
+    const u32 ls = off[blockIdx.x], n = off[blockIdx.x + 1] - ls;
+    if (n < 2) return;
+    __shared__ u32 SL[ORD_SORT_CAP];
+    const u32 tid = threadIdx.x;
+    u32 np2 = 2;
+    while (np2 < n) np2 <<= 1;
+    for (u32 i = tid; i < np2; i += SORT_T) SL[i] = i < n ? list[ls + i] : 0xFFFFFFFFu;
+    __syncthreads();
+    for (u32 k = 2; k <= np2; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            for (u32 i = tid; i < (np2 >> 1); i += SORT_T) {
+                const u32 lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;   // (lo has bit j clear)
+                const u32 a = SL[lo], b = SL[hi];
+                if ((a > b) == ((lo & k) == 0)) { SL[lo] = b; SL[hi] = a; }
+            }
+            __syncthreads();
+        }
+    for (u32 i = tid; i < n; i += SORT_T) list[ls + i] = SL[i];
 }
 
-template <bool C>
+template <bool G, bool D, bool C, bool B>
+void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s,
+                   const f64* rec, const u32* plan, hipEvent_t stop) {
+    if (fp.ipp == 4)
+        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, true, B>), dim3(ntiles), dim3(WG), 0, s, nullptr, stop, 0, fp, list,
+                              ts, te, rec, plan);
+    else
+        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, false, B>), dim3(ntiles), dim3(WG), 0, s, nullptr, stop, 0, fp,
+                              list, ts, te, rec, plan);
+}
+
+template <bool C, bool B>
 void launch_raster_c(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles,
-                     hipStream_t s, const f64* rec) {
+                     hipStream_t s, const f64* rec, const u32* plan = nullptr, hipEvent_t stop = nullptr) {
     const bool g = fp.src.gouraud != 0, d = fp.depthTest != 0;
-    if (g && d) launch_raster<true, true, C>(fp, list, ts, te, ntiles, s, rec);
-    else if (g) launch_raster<true, false, C>(fp, list, ts, te, ntiles, s, rec);
-    else if (d) launch_raster<false, true, C>(fp, list, ts, te, ntiles, s, rec);
-    else launch_raster<false, false, C>(fp, list, ts, te, ntiles, s, rec);
+    if (g && d) launch_raster<true, true, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
+    else if (g) launch_raster<true, false, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
+    else if (d) launch_raster<false, true, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
+    else launch_raster<false, false, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
 }
 
 }  // namespace
 
-void draw_ordered(RenderContext* ctx, const TriSrc& src) {
-    hipStream_t s = ctx->stream;
-    TriScratch& sc = ctx->tri;
-    FrameParams fp = frame_params(ctx, src);
-    // with a pending clear every owned tile is rasterised and written back,
-    // so the write-back also produces the frame output (as k_vis does)
-    if (ctx->frameOutput && fp.pendColor) {
-        const size_t n = (size_t)nr_frame_bytes(ctx);
-        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
-    }
-    const int ntiles = fp.tiles_x * fp.tiles_y;
+void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, hipStream_t s, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(k_tile_sort, dim3(ntiles), dim3(SORT_T), 0, s, nullptr, stop, 0, off, list, plan);
+}
 
+void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* off, const u32* plan, const f64* rec,
+                           int ntiles, hipStream_t s, hipEvent_t stop) {
+    if (fp.fragCounter) launch_raster_c<true, true>(fp, list, off, nullptr, ntiles, s, rec, plan, stop);
+    else launch_raster_c<false, true>(fp, list, off, nullptr, ntiles, s, rec, plan, stop);
+}
+
+void draw_ordered(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned) {
+    // NR_ORD_BINNED=0: always the global-sort path (A/B)
+    static const bool binned = [] {
+        const char* e = getenv("NR_ORD_BINNED");
+        return e ? atoi(e) != 0 : true;
+    }();
+    const i64 ntiles = (i64)((ctx->width + TW - 1) / TW) * ((ctx->height + TH - 1) / TH);
+    if (binned && ntiles <= ORD_BIN_TILES) {
+        draw_free(ctx, src, tb, callerOwned, true);
+        return;
+    }
+    FrameParams fp = frame_params(ctx, src);
     BinParams bp;
     bp.src = src;
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
     bp.period = fp.period; bp.mask = fp.mask;
     set_owned_rows(bp, fp.tiles_y);
+    draw_ordered_sorted(ctx, src, fp, bp);
+}
+
+// The global-sort ordered path for a batch with its state snapshot (fp, bp):
+// per-triangle tile counts -> scan -> (tile, triangle) pairs in triangle order
+// -> stable radix sort by tile -> tile ranges -> k_tile_raster.
+void draw_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParams& fp0, const BinParams& bp) {
+    hipStream_t s = ctx->stream;
+    TriScratch& sc = ctx->tri;
+    FrameParams fp = fp0;
+    const int ntiles = fp.tiles_x * fp.tiles_y;
+    // with a pending clear every owned tile is rasterised and written back,
+    // so the write-back also produces the frame output (as k_vis does)
+    if (ctx->frameOutput && fp.pendColor) {
+        const size_t n = (size_t)nr_frame_bytes(ctx);
+        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
+    }
 
     u64* tri_bufs[2] = {sc.cnt, sc.off};
     if (!grow_set(tri_bufs, &sc.tri_cap, (size_t)src.n)) return;
@@ -579,8 +597,15 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
         b.xy = src.xy + a.n * 6;
         b.z = src.z ? src.z + a.n * 3 : nullptr;
         b.rgba = src.rgba + a.n * (src.gouraud ? 12 : 4);
-        draw_ordered(ctx, a);
-        draw_ordered(ctx, b);
+        BinParams ba = bp, bb = bp;
+        ba.src = a; bb.src = b;
+        FrameParams fa = fp0, fb = fp0;
+        fa.src = a; fb.src = b;
+        draw_ordered_sorted(ctx, a, fa, ba);
+        fb.pendColor = 0;   // (the first half applied the pending clears)
+        fb.pendDepth = 0;
+        if (fb.fragCounter) NR_CHECK(hipMemsetAsync(fb.fragCounter, 0, sizeof(u64), s));
+        draw_ordered_sorted(ctx, b, fb, bb);
         return;
     }
 
@@ -618,8 +643,8 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src) {
     }
 
     nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-    if (fp.fragCounter) launch_raster_c<true>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
-    else launch_raster_c<false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
+    if (fp.fragCounter) launch_raster_c<true, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
+    else launch_raster_c<false, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
     ctx->lastPath = 2;

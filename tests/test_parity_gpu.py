@@ -208,6 +208,29 @@ def test_triangle_buffer_equals_host_arrays(gpu):
     assert_same(a, {"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, "buffer")
 
 
+@pytest.mark.parametrize("gouraud", [False, True])
+def test_ordered_tile_list_over_sort_cap(gpu, oracle, gouraud):
+    """A blended batch (ordered raster) with more triangles in one tile than
+    its per-tile LDS sort holds (ORD_SORT_CAP = 8192): the plan kernel flags it
+    and the batch takes the global-sort path -- at once for host arrays (sized
+    in the call), through the deferred re-run for a TriangleBuffer (its raster
+    was a no-op).  Flat with no Z test, Gouraud with the Z test on and write
+    off.  Same frame as the oracle either way."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    W, H = 150, 70
+    xy, z, c = scenes.triangle_soup(9000, 56, 26, 4.0, seed=71, gouraud=gouraud, alpha=(0.3, 0.7))
+    want, _ = _tri_frame(oracle, W, H, xy, z, c, depth=gouraud, write=False, alpha=True, clear=0.25)
+    got, _ = _tri_frame(gpu, W, H, xy, z, c, depth=gouraud, write=False, alpha=True, clear=0.25)
+    assert_same(got, want, "host arrays")
+    ctx = gpu.context(W, H, True)
+    for _ in range(2):   # (the second draw reuses the binning set of the first)
+        ctx.set_color(0.25, 0.25, 0.25, 0.25)
+        ctx.set_depth_state(gouraud, False)
+        ctx.clear_depth()
+        ctx.draw_triangle_buffer(R.TriangleBuffer(xy, c, z=z, gouraud=gouraud))
+        assert_same({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, want, "TriangleBuffer")
+
+
 def _grid_growth_frame(fac, W, H):
     """A tiny opaque batch, then one with ~20x its work items, in one context:
     the second batch's k_vis grid is estimated from the first (last items
