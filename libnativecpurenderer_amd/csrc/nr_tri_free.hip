@@ -1537,6 +1537,37 @@ static hipEvent_t sync_event() {
 // stream -- after the raster that last read set `si`, not after everything
 // queued before on the main stream -- so that it overlaps the previous
 // batch's k_vis (only for immutable inputs: a TriangleBuffer).
+// Device-side hand-off from the binning stream to the raster (NR_GATE=1):
+// instead of a cross-queue event wait before the raster (the main queue
+// resumed ~10-16 us after the binning finished, profiles/r03_c3/timeline_n8*),
+// the binning stream ends with k_gate_signal storing the batch's sequence
+// number, and the main queue runs k_gate_wait -- one thread polling it --
+// right before the raster, a same-queue dependency.  The wait gives up after
+// one second (a binning that never ends: the error word in the host totals,
+// host_totals[7] = seq << 32 | 1, reports it) so no wave spins forever.
+__global__ void k_gate_signal(u32* __restrict__ flag, u32 seq) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_gate_wait(const u32* __restrict__ flag, u32 seq, u64* __restrict__ host_totals) {
+    if (threadIdx.x != 0) return;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+            __hip_atomic_store(&host_totals[7], ((u64)seq << 32) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+    }
+}
+
+static bool gate_on() {
+    static const bool v = [] {
+        const char* e = getenv("NR_GATE");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
 // Host view of a plan kernel's totals (k_free_plan*): word k = (seq << 32) | value, each
 // stored by the device on its own; a batch's totals are complete once every word carries
 // its sequence number.
@@ -1753,8 +1784,18 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         nr_timing_end_on(ctx, NRK_TRI_SORT, e0, e1, sb);
     }
     if (sb != sa) {
-        if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
-        NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
+        if (gate_on()) {
+            if (!F.dgate) {
+                NR_CHECK(hipMalloc(&F.dgate, 2 * sizeof(u32)));
+                NR_CHECK(hipMemsetAsync(F.dgate, 0, 2 * sizeof(u32), sb));
+            }
+            hipLaunchKernelGGL(k_gate_signal, dim3(1), dim3(64), 0, sb, F.dgate, *seqOut);
+            hipLaunchKernelGGL(k_gate_wait, dim3(1), dim3(64), 0, sa, F.dgate, *seqOut, F.d_hplan);
+            NR_CHECK(hipGetLastError());
+        } else {
+            if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
+            NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
+        }
     }
 
     bool visDone = false;
@@ -1898,6 +1939,8 @@ void settle(RenderContext* ctx) {
             std::this_thread::yield();
         }
     }
+    if (__atomic_load_n(&F.h_plan[7], __ATOMIC_ACQUIRE) == (((u64)want << 32) | 1u))
+        nr_set_error_msg("triangle batch: the raster's wait for its binning timed out (NR_GATE)");
     sc.lastN = (u64)pb->src.n;
     sc.lastPairs = plan_val(F, 0);
     sc.lastHeavy = plan_val(F, 5);

@@ -129,8 +129,11 @@ __device__ __forceinline__ u64 window_bits(int xs, int xe) {
 // by k_tile_sort (tstart = the plan's list offsets: [off[tile], off[tile + 1]));
 // the batch is a no-op unless plan[3] (fits); otherwise [tstart, tend) of the
 // globally sorted pairs.
+#ifndef NR_ORD_WPE
+#define NR_ORD_WPE 4   // 6 (80 VGPRs, 85 spilled): C5 raster 740 -> 1355 us
+#endif
 template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA, bool BINNED>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 : NR_ORD_WPE))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
                                                     const u32* __restrict__ tstart, const u32* __restrict__ tend,
                                                     const f64* __restrict__ rec, const u32* __restrict__ plan) {
     const int tile = blockIdx.x;
@@ -272,13 +275,22 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 u64 mk[RPW];   // [j * NQ + qq]: step (4 rg % (RPW SR)) / SR + j of window qq
 #pragma unroll
                 for (int i = 0; i < RPW; ++i) mk[i] = 0;
+#ifndef NR_ORD_SPAN32
+#define NR_ORD_SPAN32 0   // 1: measured slower on C5 (786 vs 740 us, profiles/r03_c5/ab_span32_wpe.txt)
+#endif
+                // f32 crossings with an error bound (row_span32, as k_vis), the
+                // exact f64 statement for the rows the bound cannot decide
+                Span32 S32;
+                if (NR_ORD_SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = rg * 4 + r;
                     const i64 gy = y0 + row;
                     int xs = 0, xe = 0;
-                    if (ok && gy < fp.H && ymn <= (f64)gy && (f64)gy < ymx)
-                        row_span_slopes(sx, sy, sl, (f64)gy, (f64)x0, wlim, xs, xe);
+                    if (ok && gy < fp.H && ymn <= (f64)gy && (f64)gy < ymx) {
+                        if (!NR_ORD_SPAN32 || !row_span32(S32, row, (f64)gy, (float)wlim, xs, xe))
+                            row_span_slopes(sx, sy, sl, (f64)gy, (f64)x0, wlim, xs, xe);
+                    }
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
 #pragma unroll
                     for (int qq = 0; qq < NQ; ++qq)
