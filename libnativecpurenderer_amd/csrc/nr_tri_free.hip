@@ -181,14 +181,22 @@ constexpr int PLAN_T = 1024, PLAN_W = PLAN_T / 64;
 constexpr u32 HEAVY_PAIRS = 256;   // a dense tile (for the k_vis workgroup-size choice)
 constexpr int PLAN_NB = 12;
 
-// Size class of a tile's work items: 0 empty, 1 + floor(log2(count)) (capped)
-// for one slice, PLAN_NB - 1 for tiles split over several slices.  Items are
+// Size class of a tile's work items: 0 empty, 1 + the count's bin (below) for
+// one slice, PLAN_NB - 1 for tiles split over several slices.  Items are
 // laid out largest class first: k_vis workgroups take items in index order,
 // so the long ones start first and the short ones fill the tail (a longest-
 // first schedule).  Results do not depend on the order (order-free raster).
+// One-slice classes are PLAN_NB - 2 equal bins of [1, lim] (NR_CLASS_LIN=0:
+// octaves, which left a C3 frame's items -- nearly all in [256, 1024] -- in
+// two classes, in tile order within each): C3 -0.8 %, 1M tris at 1080p -1.3 %,
+// C2 -2 % per frame (profiles/r03_c3/ab_class_lin.txt).
+#ifndef NR_CLASS_LIN
+#define NR_CLASS_LIN 1
+#endif
 __device__ __forceinline__ int size_class(u32 c, u32 lim) {
     if (c > lim) return PLAN_NB - 1;
     if (c == 0) return 0;
+    if (NR_CLASS_LIN) return 1 + min((int)((float)c * ((float)(PLAN_NB - 2) / (float)(lim + 1))), PLAN_NB - 3);
     const int l = 31 - __clz(c);
     return 1 + (l < PLAN_NB - 3 ? l : PLAN_NB - 3);
 }
