@@ -1716,9 +1716,12 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         const u32 sat = sc.splitAt ? sc.splitAt : split_at(), dsl = sc.dslice ? sc.dslice : dslice();
         if ((plan_reg() && !besideRaster && ntiles <= PLAN_T * PR_MAX) || ordered) {   // (ordered: ntiles <= ORD_BIN_TILES)
             // the register plan: one 1024-thread workgroup, PR = tiles per
-            // thread -> 4, 8 or 16 (at PR 16 its tile counts, class counters and
-            // offsets take ~100 VGPRs; __launch_bounds__(1024) allows 128, so no
-            // spill).  It needs a whole CU, so beside a long raster
+            // thread -> 4, 8 or 16 (PR 4: 107 VGPRs; PR 8 and 16 spill a few,
+            // 4 and 39, at __launch_bounds__(1024)'s 128).  It needs a whole CU
+            // (an ordered batch's plan beside the ordered raster therefore waits
+            // for the raster's tail, which measured better than a 512-thread
+            // instance that runs the chain earlier, beside it: C5 +10 %,
+            // profiles/r03_c5/ab_plan512.txt), so beside a long raster
             // (besideRaster) the 256-thread, 65-VGPR multi-round k_free_plan_s
             // runs instead: it fits the slot a finishing k_vis workgroup frees
             // (C3 0.163 vs 0.172 ms; profiles/r02_c3/ab_plan_r.txt)
