@@ -13,7 +13,7 @@ OBJS = $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(SRCS))
 
 all: $(LIB) oracle
 
-$(OBJ)/%.o: $(SRC)/%.hip $(SRC)/nr_common.h $(SRC)/nr_tri.h
+$(OBJ)/%.o: $(SRC)/%.hip $(SRC)/nr_common.h $(SRC)/nr_tri.h $(SRC)/nr_tri_shade.h
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

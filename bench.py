@@ -94,15 +94,27 @@ def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True, frame_out="rgb"):
 EVENT_EVERY = 10   # timed-region frames per HIP-event-timed frame of the dominant kernel (each record pair
                    # perturbs the stream: 1 in 4 cost ~7 % of C3 throughput, 1 in 10 ~2 %)
 
-KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)"}
+KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)",
+                 "gvis_raster": "k_gvis_raster (whole-frame visibility buffer)",
+                 "gvis_resolve": "k_gvis_resolve (whole-frame visibility buffer)"}
 
 
 def kernel_bytes(cfg, n_tri, path, frac=1.0, frame_out="rgb"):
-    """Algorithmic bytes of the dominant kernel per launch.
-    Both rasterisers read each triangle (positions, depths, colours) once and
-    write the framebuffer and depth once, all inside one kernel (k_vis shades
-    its tiles itself; k_tile_raster keeps the tile in registers); k_vis also
-    writes the u8 frame (k_to_u8_rows does it after the ordered raster)."""
+    """Algorithmic bytes per launch of the path's kernels.
+    The tiled rasterisers read each triangle (positions, depths, colours) once
+    and write the framebuffer and depth once, all inside one kernel (k_vis
+    shades its tiles itself; k_tile_raster keeps the tile in registers); k_vis
+    also writes the u8 frame (k_to_u8_rows does it after the ordered raster).
+    The whole-frame visibility buffer splits the same bytes over two kernels:
+    k_gvis_raster reads every triangle's positions and depths (48 + 24 B; a
+    rank cannot know which triangles fall in its rows without reading them),
+    k_gvis_resolve the colours (96 B Gouraud / 32 B flat, the owned share) and
+    writes the owned framebuffer, depth and frame output."""
+    if path == "order-free-frame":
+        s_col = 96 if cfg["gouraud"] else 32
+        out = FRAME_OUT_BPP[frame_out]
+        return {"gvis_raster": int(n_tri * 72),
+                "gvis_resolve": int(frac * (n_tri * s_col + cfg["W"] * cfg["H"] * (8 * 3 + 4 + out)))}
     return {"tile_raster": algorithmic_bytes(cfg, n_tri, frac, u8=(path == "order-free"), frame_out=frame_out)}
 
 
@@ -123,15 +135,16 @@ def shard_tag(nsh, slots):
     return f"_shard0of{nsh}" + ("" if slots is None else "_slots" + "-".join(map(str, slots)))
 
 
-def load_pmc_traffic(cfg_name, nsh=1, slots=None, frame_out="rgb"):
+def load_pmc_traffic(cfg_name, nsh=1, slots=None, frame_out="rgb", kernel=None):
     """HBM bytes per launch of the dominant kernel from a PMC summary of the SAME
-    configuration and rank share (profiles/pmc_<config><shard tag>.json, written
-    from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes); None when there is none."""
+    configuration, rank share and kernel (profiles/pmc_<config><shard tag>.json,
+    written from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes); None when
+    there is none."""
     tag = cfg_name + shard_tag(nsh, slots) + ("" if frame_out == "rgb" else "_" + frame_out)
     p = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
     if os.path.exists(p):
         d = json.load(open(p))
-        if d.get("config") == tag:
+        if d.get("config") == tag and (kernel is None or d.get("kernel", "").startswith(kernel)):
             return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
     return None, None
 
@@ -291,7 +304,7 @@ class Runner:
         self.drain()
 
         names = ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "vis_init", "tile_raster",
-                 "resolve", "fill", "output", "gather")
+                 "gvis_raster", "gvis_resolve", "resolve", "fill", "output", "gather")
         # (1) breakdown pass: HIP events around every kernel (they add launch
         #     gaps, so this pass is not the headline)
         ctx.reset_kernel_timing()
@@ -335,12 +348,21 @@ class Runner:
         dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
         achieved = kb[dom] / (dom_us * 1e-6) / 1e9
         B = algorithmic_bytes(self.cfg, self.n_tri, frame_out=self.args.frame_output)   # whole frame
+        ksym = {"gvis_raster": "k_gvis_raster", "gvis_resolve": "k_gvis_resolve"}.get(
+            dom, "k_tile_raster" if path == "ordered" else "k_vis")
         traffic, traffic_src = load_pmc_traffic(self.cfg_name, self.nsh if self.world == 1 else 1,
-                                                slots if self.world == 1 else None, self.args.frame_output)
+                                                slots if self.world == 1 else None, self.args.frame_output, ksym)
         if self.world > 1:
             traffic, traffic_src = None, None   # per-rank PMC passes are not taken on multi-GPU runs
+        path_extra = {}
+        if len(kb) > 1:   # the whole-frame visibility buffer: both kernels' bytes over both kernels' times
+            tot_b = sum(kb.values())
+            tot_us = sum(kernels.get(k, 0.0) for k in kb)
+            if tot_us > 0:
+                path_extra = {"path_kernels": {k: {"us": kernels.get(k), "algorithmic_bytes": kb[k]} for k in kb},
+                              "path_frac": round(tot_b / (tot_us * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4)}
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
+                "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic, **path_extra,
                 "traffic_source": traffic_src or "none for this config/share (null)",
                 "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
                 "algorithmic_bytes_per_launch": kb[dom], "rank_share_of_frame": round(share, 6),

@@ -146,10 +146,11 @@ void DrawTriangleBuffer(RenderContext* ctx, TriangleBuffer* tb);         /* NEW 
 i64 GetTriangleBufferCount(TriangleBuffer* tb);                          /* NEW */
 void SetFragmentCounting(RenderContext* ctx, bool on);                   /* NEW: covered-fragment counter */
 i64 GetFragmentCount(RenderContext* ctx);                                /* NEW */
-i64 GetLastRasterPath(RenderContext* ctx);                               /* NEW: 1 order-free, 2 ordered */
+i64 GetLastRasterPath(RenderContext* ctx);                               /* NEW: 1 order-free tiled, 2 ordered, 3 order-free frame */
 void SetForceOrderedRaster(RenderContext* ctx, bool on);                 /* NEW: A/B and tests */
 void SetPairCapacityOverride(RenderContext* ctx, i64 pairs);             /* NEW: tests (0 = automatic) */
 void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW: k_vis variant 0 auto, 1 coop, 2 lane-only */
+void SetFrameVisRaster(RenderContext* ctx, i64 mode);                    /* NEW: frame visibility buffer 0 auto, 1 on, 2 off */
 void SetSplitLimits(RenderContext* ctx, i64 splitAt, i64 dslice);       /* NEW: dense-tile split limits (0: defaults) */
 
 /* ---- NEW: multi-GPU frames (tile-row sharding + RCCL assembly) */

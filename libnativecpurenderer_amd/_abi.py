@@ -82,6 +82,7 @@ DEVICE_ABI = {
     "SetForceOrderedRaster": (None, (P, B)),
     "SetPairCapacityOverride": (None, (P, L)),
     "SetCoopRaster": (None, (P, L)),
+    "SetFrameVisRaster": (None, (P, L)),
     "SetSplitLimits": (None, (P, L, L)),
     "GetLastErrorString": (ctypes.c_char_p, ()),
     "ClearLastError": (None, ()),

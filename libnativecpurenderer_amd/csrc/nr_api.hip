@@ -309,7 +309,8 @@ static void timing_collect(RenderContext* ctx) {
 
 static const char* kKernelNames[NRK_COUNT_] = {"tri_count", "tri_scan",    "tri_emit", "tri_sort",
                                                "tile_ranges", "tile_raster", "prim",     "fill",
-                                               "resolve",   "vis_init",    "output",   "gather"};
+                                               "resolve",   "vis_init",    "output",   "gather",
+                                               "gvis_raster", "gvis_resolve"};
 
 extern "C" {
 

@@ -111,30 +111,45 @@ f64* alloc_samples(i64 n, hipStream_t s) {
 // (chunk k+1's DMA in flight while chunk k is copied out on the host); the
 // host reads a chunk only after the event of its DMA.
 constexpr size_t PIN_CHUNK = 8u << 20;
+constexpr int PIN_DEVICES = 64;
 std::mutex g_pin_mu;
-void* g_pin[2] = {nullptr, nullptr};
-hipEvent_t g_pin_ev[2] = {nullptr, nullptr};
+// per device (a clip's stream belongs to the clip's device, and an event can
+// only be recorded on a stream of the device it was created on)
+struct PinPair {
+    void* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+PinPair g_pin[PIN_DEVICES];
 
+// The caller has made the clip's device current (clip_stream).
 void d2h_pinned(void* dst, const void* src, size_t bytes, hipStream_t s) {
     if (bytes == 0) return;
+    int dev = 0;
+    NR_CHECK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= PIN_DEVICES) {   // (no pinned pair: a plain synchronous copy)
+        NR_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+        NR_CHECK(hipStreamSynchronize(s));
+        return;
+    }
     std::lock_guard<std::mutex> lk(g_pin_mu);
+    PinPair& P = g_pin[dev];
     for (int k = 0; k < 2; ++k)
-        if (!g_pin[k]) {
-            NR_CHECK(hipHostMalloc(&g_pin[k], PIN_CHUNK, hipHostMallocDefault));
-            NR_CHECK(hipEventCreateWithFlags(&g_pin_ev[k], hipEventDisableTiming));
+        if (!P.buf[k]) {
+            NR_CHECK(hipHostMalloc(&P.buf[k], PIN_CHUNK, hipHostMallocDefault));
+            NR_CHECK(hipEventCreateWithFlags(&P.ev[k], hipEventDisableTiming));
         }
     const size_t nch = (bytes + PIN_CHUNK - 1) / PIN_CHUNK;
     auto issue = [&](size_t c) {
         const size_t off = c * PIN_CHUNK, len = std::min(PIN_CHUNK, bytes - off);
-        NR_CHECK(hipMemcpyAsync(g_pin[c & 1], static_cast<const iu8*>(src) + off, len, hipMemcpyDeviceToHost, s));
-        NR_CHECK(hipEventRecord(g_pin_ev[c & 1], s));
+        NR_CHECK(hipMemcpyAsync(P.buf[c & 1], static_cast<const iu8*>(src) + off, len, hipMemcpyDeviceToHost, s));
+        NR_CHECK(hipEventRecord(P.ev[c & 1], s));
     };
     issue(0);
     for (size_t c = 0; c < nch; ++c) {
         if (c + 1 < nch) issue(c + 1);   // the other buffer: its previous chunk was copied out below
-        NR_CHECK(hipEventSynchronize(g_pin_ev[c & 1]));
+        NR_CHECK(hipEventSynchronize(P.ev[c & 1]));
         const size_t off = c * PIN_CHUNK, len = std::min(PIN_CHUNK, bytes - off);
-        std::memcpy(static_cast<iu8*>(dst) + off, g_pin[c & 1], len);
+        std::memcpy(static_cast<iu8*>(dst) + off, P.buf[c & 1], len);
     }
 }
 

@@ -74,11 +74,19 @@ struct TriScratch {
     int coopMode = 0;                       // k_vis variant: 0 auto, 1 coop, 2 lane-only (SetCoopRaster)
     u32 splitAt = 0, dslice = 0;            // dense-tile split limits (SetSplitLimits; 0: NR_SPLIT_AT / NR_DSLICE)
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
+    // whole-frame visibility buffer (nr_tri_gvis.hip): W*H packed keys; state 1:
+    // every key of the owned rows of (gkeyW, gkeyH, gkeyPeriod, gkeyMask) is
+    // gkeyInit << 32; 0: unknown (the next batch initialises them)
+    u64* gkey = nullptr; size_t gkey_cap = 0;
+    int gkeyState = 0; u32 gkeyInit = 0;
+    i64 gkeyW = 0, gkeyH = 0; int gkeyPeriod = 0; u64 gkeyMask = 0;
+    int gvisMode = 0;                       // 0 automatic (NR_GVIS), 1 always, 2 never (SetFrameVisRaster)
+    f64 srcMeanArea = -1;                   // mean |signed area| of the batch being drawn, user space (-1: unknown)
 };
 
 enum NRKernelId { NRK_TRI_COUNT = 0, NRK_TRI_SCAN, NRK_TRI_EMIT, NRK_TRI_SORT, NRK_TILE_RANGES,
                   NRK_TILE_RASTER, NRK_PRIM, NRK_FILL, NRK_RESOLVE, NRK_VIS_INIT, NRK_OUTPUT, NRK_GATHER,
-                  NRK_COUNT_ };
+                  NRK_GV_RASTER, NRK_GV_RESOLVE, NRK_COUNT_ };
 
 struct RenderContext {
     i64 width = 0, height = 0;
@@ -177,6 +185,7 @@ struct TriangleBuffer {
     bool known = false;
     BinKey knownKey;
     u32 knownPairs = 0, knownHeavy = 0, knownItems = 0, knownSplit = 0;
+    f64 meanArea = -1;    // mean |signed area| of the triangles in user space (computed at upload)
 };
 
 // host helpers shared across translation units

@@ -460,6 +460,8 @@ void finish_batch(RenderContext* ctx, const FrameParams& fp);
 // of more than ORD_SORT_CAP triangles (detected by the plan, re-run)
 void draw_ordered(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned);
 void draw_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp);
+// the same kernels for a deferred re-run (nr_settle): the batch's snapshot only, context flags untouched
+void rerun_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp);
 constexpr u32 ORD_SORT_CAP = 8192;    // longest tile list the ordered raster sorts in LDS
 constexpr int ORD_BIN_TILES = 16384;  // tiles of the binned ordered path (the register plan kernel's limit)
 // binned ordered batches: k_tile_sort sorts each tile's list [off[t], off[t + 1])
@@ -474,6 +476,11 @@ void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* of
 // so the batch is sized exactly in the call -- an overflow re-run never reads
 // them after it returns
 void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned, bool ordered = false);
+// the whole-frame visibility buffer (nr_tri_gvis.hip) for opaque Z LESS + write
+// batches of small triangles: chosen per batch by gvis_wanted (objMeanArea: the
+// batch's mean |signed area| in user space, < 0 unknown)
+bool gvis_wanted(const RenderContext* ctx, const TriSrc& src, f64 objMeanArea);
+void draw_gvis(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp);
 void settle(RenderContext* ctx);
 
 }  // namespace nrtri

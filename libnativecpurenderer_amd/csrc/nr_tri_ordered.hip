@@ -556,20 +556,18 @@ void draw_ordered(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, boo
     draw_ordered_sorted(ctx, src, fp, bp);
 }
 
+namespace {
+
 // The global-sort ordered path for a batch with its state snapshot (fp, bp):
 // per-triangle tile counts -> scan -> (tile, triangle) pairs in triangle order
-// -> stable radix sort by tile -> tile ranges -> k_tile_raster.
-void draw_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParams& fp0, const BinParams& bp) {
+// -> stable radix sort by tile -> tile ranges -> k_tile_raster.  Only enqueues
+// kernels: the context's flags are the caller's business (draw_ordered_sorted
+// consumes them; a deferred re-run, rerun_ordered_sorted, must leave them as
+// the calls after the batch set them).
+void ordered_sorted_kernels(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp) {
     hipStream_t s = ctx->stream;
     TriScratch& sc = ctx->tri;
-    FrameParams fp = fp0;
     const int ntiles = fp.tiles_x * fp.tiles_y;
-    // with a pending clear every owned tile is rasterised and written back,
-    // so the write-back also produces the frame output (as k_vis does)
-    if (ctx->frameOutput && fp.pendColor) {
-        const size_t n = (size_t)nr_frame_bytes(ctx);
-        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
-    }
 
     u64* tri_bufs[2] = {sc.cnt, sc.off};
     if (!grow_set(tri_bufs, &sc.tri_cap, (size_t)src.n)) return;
@@ -611,13 +609,19 @@ void draw_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParam
         b.rgba = src.rgba + a.n * (src.gouraud ? 12 : 4);
         BinParams ba = bp, bb = bp;
         ba.src = a; bb.src = b;
-        FrameParams fa = fp0, fb = fp0;
+        FrameParams fa = fp, fb = fp;
         fa.src = a; fb.src = b;
-        draw_ordered_sorted(ctx, a, fa, ba);
+        // (fb keeps the frame output: the second half rewrites the tiles it covers)
+        ordered_sorted_kernels(ctx, a, fa, ba);
+        if (fa.fragCounter) {   // fragments of the first half, then the counter restarts for the second
+            NR_CHECK(hipMemcpyAsync(&sc.h_total[2], fa.fragCounter, sizeof(u64), hipMemcpyDeviceToHost, s));
+            NR_CHECK(hipStreamSynchronize(s));
+            ctx->fragTotal += sc.h_total[2];
+            NR_CHECK(hipMemsetAsync(fb.fragCounter, 0, sizeof(u64), s));
+        }
         fb.pendColor = 0;   // (the first half applied the pending clears)
         fb.pendDepth = 0;
-        if (fb.fragCounter) NR_CHECK(hipMemsetAsync(fb.fragCounter, 0, sizeof(u64), s));
-        draw_ordered_sorted(ctx, b, fb, bb);
+        ordered_sorted_kernels(ctx, b, fb, bb);
         return;
     }
 
@@ -659,8 +663,37 @@ void draw_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParam
     else launch_raster_c<false, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+}
+
+}  // namespace
+
+void draw_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParams& fp0, const BinParams& bp) {
+    FrameParams fp = fp0;
+    // with a pending clear every owned tile is rasterised and written back,
+    // so the write-back also produces the frame output (as k_vis does)
+    if (ctx->frameOutput && fp.pendColor) {
+        const size_t n = (size_t)nr_frame_bytes(ctx);
+        if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
+    }
+    ordered_sorted_kernels(ctx, src, fp, bp);
     ctx->lastPath = 2;
     finish_batch(ctx, fp);
+}
+
+// The deferred re-run of a batch whose binned ordered raster was a no-op (a
+// tile list over ORD_SORT_CAP, found at nr_settle): the batch's own snapshot
+// (its pending clears and frame output as they were when it was drawn), and
+// nothing of the context's current state -- the calls made since (ClearDepth,
+// SetColor, ...) have already set the flags for what comes next.  Only its
+// fragments are accounted.
+void rerun_ordered_sorted(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp) {
+    ordered_sorted_kernels(ctx, src, fp, bp);
+    if (fp.fragCounter) {
+        TriScratch& sc = ctx->tri;
+        NR_CHECK(hipMemcpyAsync(&sc.h_total[2], fp.fragCounter, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+        NR_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->fragTotal += sc.h_total[2];
+    }
 }
 
 }  // namespace nrtri

@@ -19,7 +19,9 @@ import subprocess
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+# NR_ORACLE_SO: another build of the same restatement (the ASan/UBSan one,
+# tests/test_oracle_sanitized.py)
+ORACLE_SO = os.environ.get("NR_ORACLE_SO") or os.path.join(ROOT, "oracle", "build", "liboracle.so")
 
 
 def build_oracle():
@@ -188,12 +190,16 @@ class OracleFactory:
 class GpuFactory:
     name = "gpu"
 
-    def __init__(self):
+    def __init__(self, frame_vis=0):
         from libnativecpurenderer_amd import libNativeCPURendererPybind as R
         self.R = R
+        self.frame_vis = frame_vis   # SetFrameVisRaster of every context (0: automatic)
 
     def context(self, w, h, alpha):
-        return self.R.RenderContext(w, h, alpha)
+        ctx = self.R.RenderContext(w, h, alpha)
+        if self.frame_vis:
+            ctx.set_frame_vis_raster(self.frame_vis)
+        return ctx
 
     def texture(self, arr):
         return self.R.Texture.from_numpy(arr)
@@ -206,7 +212,7 @@ class GpuRecordingFactory(GpuFactory):
     name = "gpu-recording"
 
     def context(self, w, h, alpha):
-        ctx = self.R.RenderContext(w, h, alpha)
+        ctx = super().context(w, h, alpha)
         ctx.begin_commands()
         return ctx
 

@@ -144,3 +144,29 @@ def test_random_large_frames_match_oracle(gpu, oracle, fr):
     o = _run(oracle, W, H, alpha, ops)
     for k in o:
         assert scenes.bits_equal(g[k], o[k]), (k, ops, scenes.first_mismatch(g[k], o[k]))
+
+
+@settings(max_examples=200, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(frame())
+def test_random_frames_frame_vis_match_oracle(gpu_frame, oracle, fr):
+    """The same random frames with every opaque Z LESS + write batch on the
+    whole-frame visibility buffer (k_gvis_*), whatever its triangle sizes:
+    key initialisation from a pending clear or from the depth buffer, keys
+    left for the next batch, batches of other modes in between."""
+    W, H, alpha, ops = fr
+    g = _run(gpu_frame, W, H, alpha, ops)
+    o = _run(oracle, W, H, alpha, ops)
+    for k in o:
+        assert scenes.bits_equal(g[k], o[k]), (k, ops, scenes.first_mismatch(g[k], o[k]))
+
+
+@settings(max_examples=20, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(big_frame())
+def test_random_large_frames_frame_vis_match_oracle(gpu_frame, oracle, fr):
+    W, H, alpha, ops = fr
+    g = _run(gpu_frame, W, H, alpha, ops)
+    o = _run(oracle, W, H, alpha, ops)
+    for k in o:
+        assert scenes.bits_equal(g[k], o[k]), (k, ops, scenes.first_mismatch(g[k], o[k]))

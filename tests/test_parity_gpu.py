@@ -89,11 +89,56 @@ def test_vis_variants_match_oracle(gpu, oracle, mode):
             assert_same(outs[0], outs[1], f"mode={mode} depth={depth} write={write} alpha={alpha}")
 
 
-def test_c3_gouraud_depth_4k(gpu, oracle):
+def test_c3_gouraud_depth_4k(gpu, gpu_frame, gpu_tiled, oracle):
+    """C3 at full size on both order-free rasterisers (the whole-frame
+    visibility buffer the automatic choice takes for it, and the tiled k_vis)
+    against one oracle frame."""
     xy, z, c = scenes.sphere_mesh(3840, 2160, 500, 1000)
-    g, _ = _tri_frame(gpu, 3840, 2160, xy, z, c)
     o, _ = _tri_frame(oracle, 3840, 2160, xy, z, c)
-    assert_same(g, o, "C3")
+    for fac, path in ((gpu, "order-free-frame"), (gpu_frame, "order-free-frame"), (gpu_tiled, "order-free")):
+        g, ctx = _tri_frame(fac, 3840, 2160, xy, z, c)
+        assert ctx.last_raster_path() == path
+        assert_same(g, o, "C3 " + path)
+
+
+def _gvis_state_frames(fac, W, H, parts):
+    """Frames that walk the whole-frame visibility buffer's key state: repeated
+    frames from the same pending depth clear (keys reused), a second batch in
+    the same frame (keys from the depth buffer), a clear to another depth, a
+    tiled batch in between, and a resize."""
+    a, b, c = parts
+    ctx = fac.context(W, H, False)
+    outs = []
+    for f in range(3):
+        ctx.set_color(0.2, 0.2, 0.2, 0.2)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.draw_triangles(a[0], a[2], z=a[1])
+        if f == 1:
+            ctx.draw_triangles(b[0], b[2], z=b[1])              # no pending clear: keys from the depth buffer
+        if f == 2:
+            ctx.set_depth_state(True, False)
+            ctx.draw_triangles(c[0], c[2], z=c[1])              # Z test without write (k_vis)
+            ctx.set_depth_state(True, True)
+            ctx.clear_depth(0x90000000)
+            ctx.draw_triangles(b[0], b[2], z=b[1])              # another clear value
+        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+    ctx.resize(W - 7, H + 5)
+    ctx.set_color(0.3, 0.3, 0.3, 0.3)
+    ctx.clear_depth()
+    ctx.draw_triangles(a[0], a[2], z=a[1])
+    outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+    return outs
+
+
+def test_frame_vis_key_state(gpu_frame, oracle):
+    W, H = 211, 149
+    parts = [scenes.triangle_soup(2500, W, H, s, seed=90 + k, gouraud=True, zrange=(-0.1, 1.1))
+             for k, s in enumerate((5.0, 12.0, 30.0))]
+    g = _gvis_state_frames(gpu_frame, W, H, parts)
+    o = _gvis_state_frames(oracle, W, H, parts)
+    for k, (x, y) in enumerate(zip(g, o)):
+        assert_same(x, y, f"frame {k}")
 
 
 def test_c5_blend_overdraw_reduced(gpu, oracle):
@@ -229,6 +274,64 @@ def test_ordered_tile_list_over_sort_cap(gpu, oracle, gouraud):
         ctx.clear_depth()
         ctx.draw_triangle_buffer(R.TriangleBuffer(xy, c, z=z, gouraud=gouraud))
         assert_same({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()}, want, "TriangleBuffer")
+
+
+def _overcap_then_clear_depth(fac, W, H, over, opaque_a, opaque_c, buffer):
+    """An opaque batch (writes depth), then a blended batch with a tile list
+    over ORD_SORT_CAP (a TriangleBuffer: its binned raster is a no-op that the
+    next call re-runs), then ClearDepth -- which only marks the clear pending,
+    without settling -- and another depth-writing batch, which must see the
+    cleared depth: the deferred re-run must not consume the later clear."""
+    ctx = fac.context(W, H, True)
+    ctx.set_color(0.25, 0.25, 0.25, 0.25)
+    ctx.set_depth_state(True, True)
+    ctx.clear_depth()
+    ctx.draw_triangles(opaque_a[0], opaque_a[2], z=opaque_a[1])
+    ctx.set_depth_state(True, False)
+    if buffer:
+        from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+        ctx.draw_triangle_buffer(R.TriangleBuffer(over[0], over[2], z=over[1], gouraud=True))
+    else:
+        ctx.draw_triangles(over[0], over[2], z=over[1])
+    ctx.clear_depth()
+    ctx.set_depth_state(True, True)
+    ctx.draw_triangles(opaque_c[0], opaque_c[2], z=opaque_c[1])
+    return {"f64": ctx.get_buffer_numpy(), "u8": ctx.get_buffer_as_uint8_numpy(), "depth": ctx.get_depth_buffer()}
+
+
+def test_overcap_rerun_keeps_later_depth_clear(gpu, oracle):
+    """the settle-time re-run of an over-cap ordered batch
+    used to end with the flag bookkeeping of a fresh draw (pendDepth /
+    pendColor / frameU8Valid overwritten from the old batch's snapshot)."""
+    W, H = 150, 70
+    over = scenes.triangle_soup(9000, 56, 26, 4.0, seed=71, gouraud=True, alpha=(0.3, 0.7))
+    a = scenes.triangle_soup(200, W, H, 20.0, seed=72, gouraud=True)
+    c = scenes.triangle_soup(200, W, H, 20.0, seed=73, gouraud=True)
+    want = _overcap_then_clear_depth(oracle, W, H, over, a, c, buffer=False)
+    got = _overcap_then_clear_depth(gpu, W, H, over, a, c, buffer=True)
+    assert_same(got, want, "over-cap re-run, then ClearDepth")
+
+
+def test_overcap_rerun_keeps_frame_output_stale_flag(gpu, oracle):
+    """The same re-run followed by a non-uniform SetColor (which marks the u8
+    frame mirror stale and then settles): the gathered u8 frame must be the
+    one of the new colours, not the mirror the re-run wrote."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    W, H = 150, 70
+    over = scenes.triangle_soup(9000, 56, 26, 4.0, seed=71, gouraud=False, alpha=(0.3, 0.7))
+    ctx = gpu.context(W, H, False)
+    ctx.set_color(0.5, 0.5, 0.5, 0.5)
+    ctx.gather_frame_u8()   # the frame output is produced by the rasters from now on
+    ctx.set_color(0.25, 0.25, 0.25, 0.25)
+    ctx.set_depth_state(False, False)
+    ctx.draw_triangle_buffer(R.TriangleBuffer(over[0], over[2], z=over[1], gouraud=False))
+    ctx.set_color(0.1, 0.2, 0.3, 0.9)
+    ctx.gather_frame_u8()
+    got = ctx.get_frame_u8()
+    octx = oracle.context(W, H, False)
+    octx.set_color(0.1, 0.2, 0.3, 0.9)
+    want = octx.get_buffer_as_uint8_numpy()
+    assert scenes.bits_equal(got.reshape(want.shape), want), scenes.first_mismatch(got.reshape(want.shape), want)
 
 
 def _grid_growth_frame(fac, W, H):
@@ -391,8 +494,8 @@ def _set_shard(ctx, n, r, slots):
 
 @pytest.mark.parametrize("nshards,slots", [(2, None), (3, None), (8, None), (2, [3, 1]), (3, [1, 4, 2]),
                                            (8, [5, 2, 2, 2, 2, 2, 2, 2])])
-@pytest.mark.parametrize("opaque", [True, False])
-def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque):
+@pytest.mark.parametrize("opaque,frame_vis", [(True, 2), (True, 1), (False, 0)])
+def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque, frame_vis):
     """Every shard renders only its tile rows (equal shards, or weighted
     SetShardSlots patterns); the owned rows of all shards put together are
     byte-identical to the unsharded frame (colour + depth), for both
@@ -404,6 +507,8 @@ def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque):
 
     def render(n, r):
         ctx = gpu.context(W, H, False)
+        if frame_vis:   # opaque: the tiled k_vis (2) or the whole-frame visibility buffer (1)
+            ctx.set_frame_vis_raster(frame_vis)
         _set_shard(ctx, n, r, slots if n > 1 else None)
         if n > 1:
             from libnativecpurenderer_amd import sharding
