@@ -367,11 +367,11 @@ void DestroyRenderContext(RenderContext* ctx) {
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
                     t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
-                    t.fdone,     t.kslot, t.orec};
+                    t.fdone,     t.kslot, t.orec, t.gkey};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     for (auto& F : t.fset) {
-        void* fp[] = {F.fcnt, F.foff, F.fcur, F.fitems, F.frect, F.frec, F.flist, F.dplan, F.dgate};
+        void* fp[] = {F.fcnt, F.foff, F.fcur, F.fitems, F.frect, F.frec, F.flist, F.dplan};
         for (void* p : fp)
             if (p) NR_CHECK(hipFree(p));
         if (F.h_plan) NR_CHECK(hipHostFree(F.h_plan));

@@ -57,7 +57,6 @@ struct TriScratch {
         u64* h_plan = nullptr;              // pinned, device-mapped copy of the plan totals, (seq << 32) | value
         u64* d_hplan = nullptr;             // its device address
         hipEvent_t evBin = nullptr;         // binning done (binning stream)
-        u32* dgate = nullptr;               // NR_GATE: the batch's sequence number, stored when its binning is done
         hipEvent_t evVis = nullptr;         // k_vis done reading the set (main stream)
         bool visRecorded = false;
     } fset[3];

@@ -1419,37 +1419,6 @@ static hipEvent_t sync_event() {
 // stream -- after the raster that last read set `si`, not after everything
 // queued before on the main stream -- so that it overlaps the previous
 // batch's k_vis (only for immutable inputs: a TriangleBuffer).
-// Device-side hand-off from the binning stream to the raster (NR_GATE=1):
-// instead of a cross-queue event wait before the raster (the main queue
-// resumed ~10-16 us after the binning finished, profiles/r03_c3/timeline_n8*),
-// the binning stream ends with k_gate_signal storing the batch's sequence
-// number, and the main queue runs k_gate_wait -- one thread polling it --
-// right before the raster, a same-queue dependency.  The wait gives up after
-// one second (a binning that never ends: the error word in the host totals,
-// host_totals[7] = seq << 32 | 1, reports it) so no wave spins forever.
-__global__ void k_gate_signal(u32* __restrict__ flag, u32 seq) {
-    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__global__ void k_gate_wait(const u32* __restrict__ flag, u32 seq, u64* __restrict__ host_totals) {
-    if (threadIdx.x != 0) return;
-    const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
-            __hip_atomic_store(&host_totals[7], ((u64)seq << 32) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-        }
-    }
-}
-
-static bool gate_on() {
-    static const bool v = [] {
-        const char* e = getenv("NR_GATE");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return v;
-}
-
 // Host view of a plan kernel's totals (k_free_plan*): word k = (seq << 32) | value, each
 // stored by the device on its own; a batch's totals are complete once every word carries
 // its sequence number.
@@ -1551,10 +1520,13 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         // work items: at most one per tile + one per full slice of the list,
         // twice that with dense tiles split into row halves (NR_ROW_SPLIT)
         if (!grow_items((size_t)ntiles + cap / SLICE_MIN + 2)) return ENQ_FAIL;
-        if (!grow_kslot(std::max<size_t>(std::max<size_t>((size_t)sc.lastSplit + sc.lastSplit / 4, knownSplit), 1024)))
+        // key slots of split tiles' slices (ordered batches use none): the last validated batch's + 25 %, at
+        // least one per tile (a slot per slice is needed only for tiles over the slice length)
+        if (!ordered && !grow_kslot(std::max<size_t>(std::max<size_t>((size_t)sc.lastSplit + sc.lastSplit / 4, knownSplit),
+                                                     std::min<size_t>((size_t)ntiles, 1024))))
             return ENQ_FAIL;
     } else {
-        if (!grow_list(1) || !grow_items(1) || !grow_kslot(std::max<u32>(sc.lastSplit, 1))) return ENQ_FAIL;
+        if (!grow_list(1) || !grow_items(1) || (!ordered && !grow_kslot(std::max<u32>(sc.lastSplit, 1)))) return ENQ_FAIL;
         cap = std::min<size_t>(F.flist_cap, 0xFFFFFFF0ull);
     }
 
@@ -1647,7 +1619,8 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         grid = plan_val(F, 1);
         if (plan_val(F, 3)) break;
         if (ordered && plan_val(F, 6) > ORD_SORT_CAP) return ENQ_SORTED;
-        if (attempt > 0 || !grow_list(plan_val(F, 0)) || !grow_items(plan_val(F, 1)) || !grow_kslot(plan_val(F, 2))) {
+        if (attempt > 0 || !grow_list(plan_val(F, 0)) || !grow_items(plan_val(F, 1)) ||
+            (!ordered && !grow_kslot(plan_val(F, 2)))) {
             nr_set_error_msg("triangle binning: pair list allocation failed");
             return ENQ_FAIL;
         }
@@ -1668,19 +1641,10 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_SORT, e0, e1, sb);
     }
-    if (sb != sa) {
-        if (gate_on()) {
-            if (!F.dgate) {
-                NR_CHECK(hipMalloc(&F.dgate, 2 * sizeof(u32)));
-                NR_CHECK(hipMemsetAsync(F.dgate, 0, 2 * sizeof(u32), sb));
-            }
-            hipLaunchKernelGGL(k_gate_signal, dim3(1), dim3(64), 0, sb, F.dgate, *seqOut);
-            hipLaunchKernelGGL(k_gate_wait, dim3(1), dim3(64), 0, sa, F.dgate, *seqOut, F.d_hplan);
-            NR_CHECK(hipGetLastError());
-        } else {
-            if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
-            NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
-        }
+    if (sb != sa) {   // (a device-side hand-off instead, a polling kernel on the main queue, measured +15 % on
+                      // an 8-way share and needs the two streams on separate hardware queues: removed in round 4)
+        if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
+        NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
     }
 
     bool visDone = false;
@@ -1830,8 +1794,6 @@ void settle(RenderContext* ctx) {
             std::this_thread::yield();
         }
     }
-    if (__atomic_load_n(&F.h_plan[7], __ATOMIC_ACQUIRE) == (((u64)want << 32) | 1u))
-        nr_set_error_msg("triangle batch: the raster's wait for its binning timed out (NR_GATE)");
     sc.lastN = (u64)pb->src.n;
     sc.lastPairs = plan_val(F, 0);
     sc.lastHeavy = plan_val(F, 5);
