@@ -197,8 +197,9 @@ class Runner:
     """One configuration in one context: fragment count, breakdown pass, timed
     region (K frames, barrier + synchronize on both sides, max over ranks)."""
 
-    def __init__(self, R, args, cfg_name, world, rank, dist, rdev, nsh, me, deliver="none"):
+    def __init__(self, R, args, cfg_name, world, rank, dist, rdev, nsh, me, deliver="none", frame_output=None):
         self.R, self.args, self.cfg_name = R, args, cfg_name
+        self.frame_output = frame_output or args.frame_output
         self.cfg = CONFIGS[cfg_name]
         self.world, self.rank, self.dist, self.rdev = world, rank, dist, rdev
         self.nsh, self.me, self.deliver = nsh, me, deliver
@@ -207,7 +208,7 @@ class Runner:
         self.xy, self.z, self.c = make_scene(cfg)
         self.n_tri = len(self.xy)
         self.ctx = R.RenderContext(self.W, self.H, False)
-        self.ctx.set_frame_format(args.frame_output)
+        self.ctx.set_frame_format(self.frame_output)
         if args.force_ordered:
             self.ctx.set_force_ordered_raster(True)
         self.buf = R.TriangleBuffer(self.xy, self.c, z=self.z, gouraud=cfg["gouraud"])
@@ -323,7 +324,7 @@ class Runner:
         from libnativecpurenderer_amd import sharding
         slots = self.slots_for(self.root_k) if self.nsh > 1 else None
         share = len(sharding.owned_rows(self.H, self.nsh, self.me, slots=slots)) / self.H
-        kb = kernel_bytes(self.cfg, self.n_tri, path, share, self.args.frame_output)
+        kb = kernel_bytes(self.cfg, self.n_tri, path, share, self.frame_output)
         dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
         # (2) timed region: K frames, HIP events only around the dominant kernel
@@ -347,11 +348,11 @@ class Runner:
         tot, cnt = ctx.get_kernel_timing(dom)
         dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
         achieved = kb[dom] / (dom_us * 1e-6) / 1e9
-        B = algorithmic_bytes(self.cfg, self.n_tri, frame_out=self.args.frame_output)   # whole frame
+        B = algorithmic_bytes(self.cfg, self.n_tri, frame_out=self.frame_output)   # whole frame
         ksym = {"gvis_raster": "k_gvis_raster", "gvis_resolve": "k_gvis_resolve"}.get(
             dom, "k_tile_raster" if path == "ordered" else "k_vis")
         traffic, traffic_src = load_pmc_traffic(self.cfg_name, self.nsh if self.world == 1 else 1,
-                                                slots if self.world == 1 else None, self.args.frame_output, ksym)
+                                                slots if self.world == 1 else None, self.frame_output, ksym)
         if self.world > 1:
             traffic, traffic_src = None, None   # per-rank PMC passes are not taken on multi-GPU runs
         path_extra = {}
@@ -451,14 +452,17 @@ def main():
     extra = {}
     do_extra = args.extra if args.extra is not None else (world == 1 and nsh == 1)
     if do_extra and world == 1:
-        jobs = [("c3_1080p", "none"), ("c2", "none"), ("c5", "none"), (args.config, "host"), ("c2", "host")]
-        for name, dl in jobs:
-            if name == args.config and dl == args.deliver:
+        jobs = [("c3_1080p", "none", None), ("c2", "none", None), ("c5", "none", None), (args.config, "host", None),
+                (args.config, "host", "yuv420p"), ("c2", "host", None)]
+        for name, dl, fo in jobs:
+            if name == args.config and dl == args.deliver and (fo or args.frame_output) == args.frame_output:
                 continue
-            sub = Runner(R, args, name, 1, 0, None, rdev, nsh, 0, dl)
+            sub = Runner(R, args, name, 1, 0, None, rdev, nsh, 0, dl, fo)
             r = sub.run(args.steps, args.warmup)
-            key = name + ("_host_delivered" if dl == "host" else "")
-            extra[key] = {"workload": sub.cfg["desc"] + (" + frame output delivered to host memory" if dl == "host" else ""),
+            key = name + ("_host_delivered" if dl == "host" else "") + ("_" + fo if fo else "")
+            what = (" + frame output (" + ("YUV420P planes, the encoder's input" if sub.frame_output == "yuv420p"
+                                           else "u8 RGB image") + ") delivered to host memory") if dl == "host" else ""
+            extra[key] = {"workload": sub.cfg["desc"] + what,
                           "triangles": sub.n_tri, **{k: r[k] for k in ("value", "ms_per_step", "fps",
                                                                          "fragments_per_frame", "roofline",
                                                                          "raster_path", "kernel_us")},
@@ -468,6 +472,12 @@ def main():
                 same = res if name == args.config and args.deliver == "none" else extra.get(name)
                 extra[key]["in_hbm_ms_per_step"] = same["ms_per_step"] if same else None
             del sub
+        # the real caller's frame: milrenderer's primitive mix (milrenderer.py:865-1038) through the deferred
+        # command list, with its frame handed over as YUV420P in host memory, beside the oracle
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_mil
+        extra["milrenderer_command_list"] = bench_mil.run(frames=max(10, min(args.steps, 50)),
+                                                          oracle=not args.no_cpu_baseline)
 
     if rank != 0:
         return

@@ -8,7 +8,8 @@ import os
 
 from . import _abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libNativeCPURenderer.so")
+# NR_LIB: another build of the same library (A/B and check builds under tools/exp only)
+LIB_PATH = os.environ.get("NR_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libNativeCPURenderer.so")
 
 _lib = None
 

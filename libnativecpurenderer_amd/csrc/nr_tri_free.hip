@@ -857,6 +857,10 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
             if (cur == 0) break;
         }
         f64 cr, cg, cb, ca;
+        NR_DEV_CHECK(d >= St::RT || (u32)d < U, "shade_tile: pixel (%ld, %ld) reads record %d of %u staged (winner %u)",
+                     (long)px, (long)py, d, U, id);
+        NR_DEV_CHECK(id <= (u32)fp.src.n, "shade_tile: pixel (%ld, %ld) winner %u of %ld triangles", (long)px, (long)py, id,
+                     (long)fp.src.n);
         if (d < St::RT) {
             record_colour<GOURAUD>(rec + d * St::REC, px, py, cr, cg, cb, ca);
         } else if (OVF_Q) {

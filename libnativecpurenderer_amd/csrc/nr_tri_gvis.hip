@@ -174,6 +174,8 @@ __global__ __launch_bounds__(GV_RT) void k_gvis_resolve(const FrameParams fp, co
             }
             continue;
         }
+        NR_DEV_CHECK(id <= (u32)fp.src.n, "gvis_resolve: pixel (%ld, %ld) winner %u of %ld triangles", (long)px,
+                     (long)y, id, (long)fp.src.n);
         if (id != have) {
             make_record<GOURAUD>(fp, (i64)id - 1, rec);
             have = id;

@@ -9,6 +9,23 @@
 
 #include "nr_tri.h"
 
+// Index checks of the shading passes (a build with -DNR_SHADE_CHECK=1 only:
+// tools/exp/check.so, loaded with NR_LIB=...): a failed check prints the
+// pixel and the indices instead of reading out of range silently.
+#ifndef NR_SHADE_CHECK
+#define NR_SHADE_CHECK 0
+#endif
+#if NR_SHADE_CHECK
+#define NR_DEV_CHECK(cond, ...)                       \
+    do {                                              \
+        if (!(cond)) printf("NR_SHADE_CHECK " __VA_ARGS__); \
+    } while (0)
+#else
+#define NR_DEV_CHECK(cond, ...) \
+    do {                        \
+    } while (0)
+#endif
+
 namespace nrtri {
 
 // Doubles of a shading record (build_record): Gouraud sx0 sy0 e1x e1y e2x e2y

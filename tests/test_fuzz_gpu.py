@@ -170,3 +170,31 @@ def test_random_large_frames_frame_vis_match_oracle(gpu_frame, oracle, fr):
     o = _run(oracle, W, H, alpha, ops)
     for k in o:
         assert scenes.bits_equal(g[k], o[k]), (k, ops, scenes.first_mismatch(g[k], o[k]))
+
+
+# Round 3 dropped a shading variant after it produced NaN pixels on this frame
+# (replayed example 34 of tools/fuzz_examples.json: a 1x58 RGB frame, 58 opaque
+# Gouraud triangles, no depth test).  Kept as a regression case with its
+# neighbours: 1-pixel-wide and 1-pixel-high frames in every depth mode, on both
+# order-free rasterisers and the ordered one.
+NARROW = [(1, 58, False, [("tri", 58, 1478763101, 1.5, True, False, False, False)])] + [
+    (w, h, a, [("tri", n, 7000 + k, s, g, b, t, wr)])
+    for k, (w, h, a, n, s, g, b, t, wr) in enumerate([
+        (1, 58, False, 58, 1.5, True, False, True, True),
+        (1, 58, True, 200, 6.0, True, False, True, False),
+        (1, 97, False, 300, 1.5, False, False, True, True),
+        (2, 70, False, 120, 40.0, True, True, True, False),
+        (77, 1, False, 90, 1.5, True, False, True, True),
+        (130, 1, True, 90, 6.0, False, False, False, False),
+        (1, 1, False, 10, 1.5, True, False, True, True),
+    ])]
+
+
+@pytest.mark.parametrize("k", range(len(NARROW)))
+def test_narrow_frames_match_oracle(gpu, gpu_frame, gpu_tiled, oracle, k):
+    W, H, alpha, ops = NARROW[k]
+    o = _run(oracle, W, H, alpha, ops)
+    for fac in (gpu, gpu_frame, gpu_tiled):
+        g = _run(fac, W, H, alpha, ops)
+        for key in o:
+            assert scenes.bits_equal(g[key], o[key]), (fac.frame_vis, key, scenes.first_mismatch(g[key], o[key]))

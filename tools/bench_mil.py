@@ -73,32 +73,51 @@ class Counter:
     def draw_vertical_mut_grd(self, x, y, w, h, steps): self.n += len(steps) - 1
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=30)
-    ap.add_argument("--no-oracle", action="store_true")
-    args = ap.parse_args()
+def run(frames=30, oracle=True):
+    """One JSON-able dict: ms per frame for immediate calls, the recorded
+    command list, the recorded list with the frame handed to the video
+    caller (YUV420P planes, PutRendererContextFrame's input, cpp:232-275,
+    delivered to host memory, D2H overlapped with the next frame), and the
+    CPU oracle; the recorded frame checked against the oracle bit for bit."""
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     gpu = scenes.GpuFactory()
     tx = make_textures(gpu)
     cnt = Counter()
     frame(cnt, {k: None for k in tx}, 0.0)
-    res = {"workload": "milrenderer-style frame 1920x1080 RGB", "draws_per_frame": cnt.n}
-    for mode in ("immediate", "recorded"):
+    res = {"workload": "milrenderer-style frame 1920x1080 RGB (milrenderer.py:865-1038 primitive mix)",
+           "draws_per_frame": cnt.n}
+    g = None
+    for mode in ("immediate", "recorded", "recorded_yuv420p_to_host"):
         ctx = R.RenderContext(W, H, False)
-        if mode == "recorded":
+        host, tickets = None, []
+        if mode != "immediate":
             ctx.begin_commands()
-        for i in range(3):
-            frame(ctx, tx, i * 0.1)
-            ctx.flush_commands() if mode == "recorded" else None
-        ctx.flush()
-        t0 = time.perf_counter()
-        for i in range(args.frames):
-            frame(ctx, tx, i * 0.1)
-            if mode == "recorded":
+        if mode == "recorded_yuv420p_to_host":
+            ctx.set_frame_format("yuv420p")
+            host = [R.HostBuffer(int(np.prod(ctx.frame_output_shape()))) for _ in range(2)]
+
+        def one(i, t):
+            frame(ctx, tx, t)
+            if mode != "immediate":
                 ctx.flush_commands()
+            if host is not None:
+                ctx.gather_frame_u8()
+                if len(tickets) >= 2:
+                    ctx.wait_frame_delivered(tickets.pop(0))
+                tickets.append(ctx.deliver_frame(host[i % 2]))
+
+        for i in range(3):
+            one(i, i * 0.1)
         ctx.flush()
-        dt = (time.perf_counter() - t0) / args.frames
+        while tickets:
+            ctx.wait_frame_delivered(tickets.pop(0))
+        t0 = time.perf_counter()
+        for i in range(frames):
+            one(i, i * 0.1)
+        ctx.flush()
+        while tickets:
+            ctx.wait_frame_delivered(tickets.pop(0))
+        dt = (time.perf_counter() - t0) / frames
         res[f"{mode}_ms_per_frame"] = round(dt * 1e3, 3)
         if mode == "recorded":
             ctx.enable_kernel_timing(True)
@@ -110,7 +129,7 @@ def main():
             ctx.enable_kernel_timing(False)
             frame(ctx, tx, 0.7)
             g = ctx.get_buffer_numpy()
-    if not args.no_oracle:
+    if oracle:
         of = scenes.OracleFactory()
         otx = make_textures(of)
         octx = of.context(W, H, False)
@@ -118,8 +137,17 @@ def main():
         frame(octx, otx, 0.7)
         o = octx.get_buffer_numpy()
         res["oracle_ms_per_frame"] = round((time.perf_counter() - t0) * 1e3, 1)
+        res["oracle_note"] = "CPU oracle (oracle/oracle.c, 1 thread), the same frame's draws; no frame output"
         res["recorded_bit_exact_vs_oracle"] = bool(scenes.bits_equal(g, o))
-    print(json.dumps(res))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=30)
+    ap.add_argument("--no-oracle", action="store_true")
+    args = ap.parse_args()
+    print(json.dumps(run(args.frames, not args.no_oracle)))
 
 
 if __name__ == "__main__":

@@ -34,7 +34,7 @@ for step in "$@"; do
   [ "$kind" != "$step" ] && arg=${step#*:}
   IFS=',' read -r -a A <<< "$arg"
   case $kind in
-    test)  run test 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ${A[@]} ;;
+    test)  run test 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread "${A[@]}" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py "${A[@]}" ;;
     trace) d="$OUT/trace$i"
