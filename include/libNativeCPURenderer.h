@@ -151,6 +151,8 @@ void SetForceOrderedRaster(RenderContext* ctx, bool on);                 /* NEW:
 void SetPairCapacityOverride(RenderContext* ctx, i64 pairs);             /* NEW: tests (0 = automatic) */
 void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW: k_vis variant 0 auto, 1 coop, 2 lane-only */
 void SetFrameVisRaster(RenderContext* ctx, i64 mode);                    /* NEW: frame visibility buffer 0 auto, 1 on, 2 off */
+void SetWarmBinning(RenderContext* ctx, i64 mode);                       /* NEW: one-pass binning of a repeat draw 0 auto, 1 on, 2 off */
+i64 GetWarmBatchCount(RenderContext* ctx);                               /* NEW (testing): batches binned warm */
 void SetSplitLimits(RenderContext* ctx, i64 splitAt, i64 dslice);       /* NEW: dense-tile split limits (0: defaults) */
 
 /* ---- NEW: multi-GPU frames (tile-row sharding + RCCL assembly) */

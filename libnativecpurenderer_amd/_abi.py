@@ -83,6 +83,8 @@ DEVICE_ABI = {
     "SetPairCapacityOverride": (None, (P, L)),
     "SetCoopRaster": (None, (P, L)),
     "SetFrameVisRaster": (None, (P, L)),
+    "SetWarmBinning": (None, (P, L)),
+    "GetWarmBatchCount": (L, (P,)),
     "SetSplitLimits": (None, (P, L, L)),
     "GetLastErrorString": (ctypes.c_char_p, ()),
     "ClearLastError": (None, ()),

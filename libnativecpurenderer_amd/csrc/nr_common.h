@@ -32,9 +32,19 @@ void nr_set_error_msg(const char* msg);
 // host objects
 // ---------------------------------------------------------------------------
 struct NRState { f64 m[6]; f64 ct[4]; };
+typedef unsigned long long u64;
+
+// Binning geometry of a draw: the positions' transform, the frame and the
+// owned tile rows.  The same buffer binned under the same key gives the same
+// (tile, triangle) pairs, work items and dense tiles.
+struct BinKey {
+    f64 m[6];
+    i64 W, H;
+    int period;
+    u64 mask;
+};
 
 // Scratch of the triangle pipeline, grown on demand (never shrunk).
-typedef unsigned long long u64;
 struct TriScratch {
     u64* cnt = nullptr; u64* off = nullptr; size_t tri_cap = 0;          // per triangle
     f64* orec = nullptr; size_t orec_cap = 0;   // ordered raster: per-triangle setup records (ORec doubles each)
@@ -59,6 +69,7 @@ struct TriScratch {
         hipEvent_t evBin = nullptr;         // binning done (binning stream)
         hipEvent_t evVis = nullptr;         // k_vis done reading the set (main stream)
         bool visRecorded = false;
+        bool curClean = false;              // fcur all zero (a warm batch's k_vis re-zeroed it; a cold one leaves counts)
     } fset[3];
     int fnext = 0;                          // set of the next batch
     u32* fdone = nullptr; size_t fdone_cap = 0;   // split-tile slice counters (k_vis only)
@@ -80,6 +91,26 @@ struct TriScratch {
     int gkeyState = 0; u32 gkeyInit = 0;
     i64 gkeyW = 0, gkeyH = 0; int gkeyPeriod = 0; u64 gkeyMask = 0;
     int gvisMode = 0;                       // 0 automatic (NR_GVIS), 1 always, 2 never (SetFrameVisRaster)
+    // warm binning (nr_tri_free.hip): the tile offsets, k_vis work items and
+    // plan totals of the last validated binning of one TriangleBuffer under
+    // one binning key -- a later draw of the same buffer under the same key
+    // has the same (tile, triangle) pairs, so it bins in one pass into these
+    // ranges (no count pass, no plan, no validation)
+    struct Schedule {
+        bool valid = false;
+        u64 tbUid = 0;
+        BinKey key;
+        u32* off = nullptr; size_t off_cap = 0;          // ntiles + 1 list offsets
+        uint4* items = nullptr; size_t items_cap = 0;    // k_vis work items
+        u32* dplan = nullptr;                            // the plan's device totals {pairs, items, slices, fits}
+        u32 pairs = 0, nitems = 0, heavy = 0, split = 0;
+        u64 n = 0;
+        hipEvent_t ready = nullptr;                      // the copies above are done (main stream)
+        bool waitReady = false;                          // the next warm binning on the binning stream waits for it
+        u32* herr = nullptr; u32* derr = nullptr;        // host-mapped: a warm binning found a tile over its range
+    } sched;
+    int warmMode = 0;                       // 0 automatic (NR_WARM), 1 on, 2 off (SetWarmBinning)
+    u64 warmBatches = 0;                    // batches binned warm (GetWarmBatchCount)
     f64 srcMeanArea = -1;                   // mean |signed area| of the batch being drawn, user space (-1: unknown)
 };
 
@@ -161,16 +192,6 @@ struct Texture {
     int device = 0;
 };
 
-// Binning geometry of a draw: the positions' transform, the frame and the
-// owned tile rows.  The same buffer binned under the same key gives the same
-// (tile, triangle) pairs, work items and dense tiles.
-struct BinKey {
-    f64 m[6];
-    i64 W, H;
-    int period;
-    u64 mask;
-};
-
 struct TriangleBuffer {
     i64 n = 0;
     bool gouraud = false;
@@ -185,6 +206,7 @@ struct TriangleBuffer {
     BinKey knownKey;
     u32 knownPairs = 0, knownHeavy = 0, knownItems = 0, knownSplit = 0;
     f64 meanArea = -1;    // mean |signed area| of the triangles in user space (computed at upload)
+    u64 uid = 0;          // process-unique id (a context's warm schedule names its buffer by it)
 };
 
 // host helpers shared across translation units

@@ -9,6 +9,7 @@
 #include "nr_tri.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 
 namespace nrtri {
@@ -229,7 +230,9 @@ void DrawTriangles(RenderContext* ctx, const f64* xy, const f64* z, const f64* r
 
 // New: a device-resident triangle soup (the H2D point; drawn many times).
 TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f64* rgba, bool gouraud) {
+    static std::atomic<u64> g_uid{0};
     TriangleBuffer* tb = new TriangleBuffer();
+    tb->uid = ++g_uid;
     tb->n = n;
     tb->gouraud = gouraud;
     tb->opaque = n > 0 && host_opacity(rgba, n, gouraud) == OPQ_OPAQUE;
@@ -285,6 +288,13 @@ i64 GetFragmentCount(RenderContext* ctx) { return (i64)ctx->fragTotal; }
 // opaque Z LESS + write batches, 0 automatic (small triangles, NR_GVIS), 1
 // every such batch, 2 never (the tiled k_vis path).
 void SetFrameVisRaster(RenderContext* ctx, i64 mode) { ctx->tri.gvisMode = (int)(mode >= 0 && mode <= 2 ? mode : 0); }
+
+// New (testing / A-B measurement): warm binning of a TriangleBuffer drawn
+// again under the key of its last validated binning (one binning pass into
+// the kept tile ranges), 0 automatic (NR_WARM), 1 on, 2 off.
+void SetWarmBinning(RenderContext* ctx, i64 mode) { ctx->tri.warmMode = (int)(mode >= 0 && mode <= 2 ? mode : 0); }
+// New (testing): number of batches of this context binned warm so far.
+i64 GetWarmBatchCount(RenderContext* ctx) { return (i64)ctx->tri.warmBatches; }
 
 // New: which raster the last batch took (1 = order-free tiled, 2 = ordered, 3 = order-free frame buffer).
 i64 GetLastRasterPath(RenderContext* ctx) { return ctx->lastPath; }

@@ -648,6 +648,96 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
     }
 }
 
+// Warm binning: a TriangleBuffer drawn again under the binning key of its
+// last validated binning, whose tile offsets and work items the context keeps
+// (TriScratch::Schedule).  One pass over the triangles -- screen rectangle
+// (as k_free_count), the workgroup's LDS histogram of its pairs over the owned
+// tile rows, one range reservation per touched tile, the pairs (as
+// k_free_emit) -- into the same [off[t], off[t + 1]) ranges: the count pass,
+// the plan and the host's validation of the cold path are not needed,
+// because the same buffer under the same key gives every tile exactly its
+// former count.  (A tile found over its range -- not possible -- sets *err and
+// its excess pairs are dropped.)  LDSH: hist (next slot) and hlim (range end)
+// per owned tile in LDS.
+template <bool LDSH>
+__global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32* __restrict__ off,
+                                                  u32* __restrict__ cur, u32* __restrict__ list,
+                                                  u32* __restrict__ err) {
+    extern __shared__ u32 hist[];
+    const int tid = threadIdx.x;
+    const i64 base = (i64)blockIdx.x * 256 * TPT;
+    const int hbins = bp.hrows * bp.tiles_x;
+    u32* hlim = hist + hbins;
+    f64 pxy[TPT][6];
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
+    }
+    if (LDSH) {
+        for (int b = tid; b < hbins; b += 256) hist[b] = 0;
+        __syncthreads();
+    }
+    u64 rk[TPT];
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        rk[k] = NO_RECT;
+        if (t >= bp.src.n) continue;
+        f64 sx[3], sy[3];
+#pragma unroll
+        for (int v = 0; v < 3; ++v) nr_xform(bp.m, pxy[k][2 * v], pxy[k][2 * v + 1], sx[v], sy[v]);
+        int tx0, tx1, ty0, ty1;
+        if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
+        rk[k] = pack_rect(tx0, tx1, ty0, ty1);
+        if (!LDSH) continue;
+        for (int ty = ty0; ty <= ty1; ++ty) {
+            if (!owned_row(ty, bp.period, bp.mask)) continue;
+            const int hrow = owned_ord(bp, ty) * bp.tiles_x;
+            for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[hrow + tx], 1u);
+        }
+    }
+    if (LDSH) {
+        __syncthreads();
+        for (int b = tid; b < hbins; b += 256) {   // reserve each touched tile's range once
+            const u32 h = hist[b];
+            if (h) {
+                const int r = b / bp.tiles_x;
+                const int tile = owned_row_of(bp, r) * bp.tiles_x + (b - r * bp.tiles_x);
+                const u32 start = off[tile] + atomicAdd(&cur[tile], h), end = off[tile + 1];
+                hist[b] = start;
+                hlim[b] = end;
+                if (start + h > end) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        const u64 rc = rk[k];
+        if (t >= bp.src.n || rc == NO_RECT) continue;
+        const int tx0 = (int)(rc & 0xFFFF), tx1 = (int)((rc >> 16) & 0xFFFF);
+        const int ty0 = (int)((rc >> 32) & 0xFFFF), ty1 = (int)(rc >> 48);
+        for (int ty = ty0; ty <= ty1; ++ty) {
+            if (!owned_row(ty, bp.period, bp.mask)) continue;
+            const int hrow = (LDSH ? owned_ord(bp, ty) : ty) * bp.tiles_x;
+            for (int tx = tx0; tx <= tx1; ++tx) {
+                u32 slot, end;
+                if (LDSH) {
+                    slot = atomicAdd(&hist[hrow + tx], 1u);
+                    end = hlim[hrow + tx];
+                } else {
+                    slot = off[hrow + tx] + atomicAdd(&cur[hrow + tx], 1u);
+                    end = off[hrow + tx + 1];
+                    if (slot >= end) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                if (slot < end) list[slot] = (u32)t;
+            }
+        }
+    }
+}
+
 // ---- deferred shading --------------------------------------------------
 // A workgroup shades its tile after the raster.  The winners of the tile's
 // pixels are few (a triangle wins ~9 pixels of the C3 mesh), so they are
@@ -965,7 +1055,7 @@ template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT, int WPE = NR_V
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ kslot, u32* __restrict__ done,
-                                             const u32* __restrict__ plan) {
+                                             const u32* __restrict__ plan, u32* __restrict__ zcur) {
     constexpr bool DEPTH = ZMODE != 0;
     constexpr int NWV = NT / 64;   // waves per workgroup
     // tile keys, rows padded to KS = 65 entries: lanes working on different
@@ -1005,6 +1095,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (le - ls >= (u32)NR_HEAVY_PRIO) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(NR_VIS_BASE_PRIO);
 #endif
+        // warm binning (zcur): the tile's pair cursor goes back to zero for the
+        // binning that next uses this set (every owned tile has an item; a
+        // tile's first slice does it: the binning that counted is done)
+        if (zcur && tid == 0 && (d.w >> 16) == 0) zcur[tile] = 0;
         const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
@@ -1284,8 +1378,18 @@ static bool vis_wpe3(bool big) {
     return v >= 0 ? v != 0 : big;
 }
 
+// The k_vis inputs of one batch: its work items, pair list and plan totals
+// (a binning set's, or the warm schedule's), and the pair cursors a warm
+// batch's k_vis re-zeroes (null otherwise).
+struct VisArgs {
+    const uint4* items;
+    const u32* list;
+    const u32* plan;
+    u32* zcur;
+};
+
 template <int Z, bool C, bool G>
-void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid, hipStream_t s,
+void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
                 hipEvent_t stop, bool big) {
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
@@ -1294,34 +1398,35 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const TriScratch::F
     // wide workgroups when the last batch had few pairs (a sharded frame):
     // its dense items run at low occupancy and are latency-bound
     const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wide_heavy();
+#define NR_VIS(CO, NTT, ...)                                                                                       \
+    hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, nullptr, stop, 0, fp, va.items,  \
+                          va.list, sc.kslot, sc.fdone, va.plan, va.zcur)
     if (wide) {
-        if (coop)
-            hipExtLaunchKernelGGL((k_vis<Z, false, G, true, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, nullptr, stop, 0, fp, F.fitems,
-                               F.flist, sc.kslot, sc.fdone, F.dplan);
-        else
-            hipExtLaunchKernelGGL((k_vis<Z, false, G, false, 2 * VWG>), dim3(grid), dim3(2 * VWG), 0, s, nullptr, stop, 0, fp, F.fitems,
-                               F.flist, sc.kslot, sc.fdone, F.dplan);
+        if (coop) NR_VIS(1, 2 * VWG, false, G, true, 2 * VWG);
+        else NR_VIS(0, 2 * VWG, false, G, false, 2 * VWG);
     } else if (!C && vis_wpe3(big)) {
-        if (coop)
-            hipExtLaunchKernelGGL((k_vis<Z, false, G, true, VWG, 3>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp,
-                                  F.fitems, F.flist, sc.kslot, sc.fdone, F.dplan);
-        else
-            hipExtLaunchKernelGGL((k_vis<Z, false, G, false, VWG, 3>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp,
-                                  F.fitems, F.flist, sc.kslot, sc.fdone, F.dplan);
+        if (coop) NR_VIS(1, VWG, false, G, true, VWG, 3);
+        else NR_VIS(0, VWG, false, G, false, VWG, 3);
     } else if (coop) {
-        hipExtLaunchKernelGGL((k_vis<Z, C, G, true, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.kslot,
-                           sc.fdone, F.dplan);
+        NR_VIS(1, VWG, C, G, true, VWG);
     } else {
-        hipExtLaunchKernelGGL((k_vis<Z, C, G, false, VWG>), dim3(grid), dim3(VWG), 0, s, nullptr, stop, 0, fp, F.fitems, F.flist, sc.kslot,
-                           sc.fdone, F.dplan);
+        NR_VIS(0, VWG, C, G, false, VWG);
     }
+#undef NR_VIS
 }
 
 template <int Z, bool G>
-void launch_vis_z(const FrameParams& fp, const TriScratch& sc, const TriScratch::FreeSet& F, u32 grid,
-                  hipStream_t s, hipEvent_t stop, bool big) {
-    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, F, grid, s, stop, big);
-    else launch_vis<Z, false, G>(fp, sc, F, grid, s, stop, big);
+void launch_vis_z(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
+                  hipEvent_t stop, bool big) {
+    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, va, grid, s, stop, big);
+    else launch_vis<Z, false, G>(fp, sc, va, grid, s, stop, big);
+}
+
+static void launch_vis_any(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
+                           hipEvent_t stop, bool big, int zmode, bool g) {
+    if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, va, grid, s, stop, big); else launch_vis_z<1, false>(fp, sc, va, grid, s, stop, big); }
+    else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, va, grid, s, stop, big); else launch_vis_z<2, false>(fp, sc, va, grid, s, stop, big); }
+    else { if (g) launch_vis_z<0, true>(fp, sc, va, grid, s, stop, big); else launch_vis_z<0, false>(fp, sc, va, grid, s, stop, big); }
 }
 
 // Events of a batch carried by the kernels' own completion signals
@@ -1664,9 +1769,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         const bool vs = ext_stop() && !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
         const bool largeShare = owned_share_large(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
-        if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<1, false>(fp, sc, F, grid, sa, st, largeShare); }
-        else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<2, false>(fp, sc, F, grid, sa, st, largeShare); }
-        else { if (g) launch_vis_z<0, true>(fp, sc, F, grid, sa, st, largeShare); else launch_vis_z<0, false>(fp, sc, F, grid, sa, st, largeShare); }
+        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, nullptr}, grid, sa, st, largeShare, zmode, g);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
@@ -1674,6 +1777,152 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
     F.visRecorded = true;
     return ENQ_OK;
+}
+
+// ---- warm binning ---------------------------------------------------------
+// NR_WARM: 0 off, 1 on (default); NR_WARM_INLINE: 1 bin a warm batch on the
+// main stream right before its raster (no cross-queue wait), 0 on the
+// binning stream beside the previous raster.
+static bool warm_on(const TriScratch& sc) {
+    static const int v = [] {
+        const char* e = getenv("NR_WARM");
+        return e ? atoi(e) : 1;
+    }();
+    return sc.warmMode ? sc.warmMode == 1 : v != 0;
+}
+static bool warm_inline() {
+    static const bool v = [] {
+        const char* e = getenv("NR_WARM_INLINE");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
+// Keeps the tile offsets, work items and plan totals of a validated binning
+// of `tb` under `key` (binning set F, which held room for them) as the
+// context's warm schedule: device copies on the main stream, after the
+// batch's raster; the set's next binning waits for them (F.evVis).
+static void sched_capture(RenderContext* ctx, TriScratch::FreeSet& F, const BinKey& key, const TriangleBuffer* tb,
+                          int ntiles, u32 pairs, u32 items, u32 heavy, u32 split, u64 n) {
+    TriScratch& sc = ctx->tri;
+    if (!warm_on(sc) || !tb) return;
+    auto& S = sc.sched;
+    hipStream_t sa = ctx->stream;
+    S.valid = false;
+    if (S.off_cap < (size_t)ntiles + 1 || S.items_cap < std::max<size_t>(items, 1) || !S.dplan) {
+        NR_CHECK(hipStreamSynchronize(sa));   // a queued warm batch may still read the old arrays
+        NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
+        u32* ob[1] = {S.off};
+        if (!grow_set(ob, &S.off_cap, (size_t)ntiles + 1)) return;
+        S.off = ob[0];
+        uint4* ib[1] = {S.items};
+        if (!grow_set(ib, &S.items_cap, std::max<size_t>(items, 1))) return;
+        S.items = ib[0];
+        if (!S.dplan) NR_CHECK(hipMalloc(&S.dplan, 4 * sizeof(u32)));
+    }
+    if (!S.ready) S.ready = sync_event();
+    if (!S.herr) {
+        NR_CHECK(hipHostMalloc((void**)&S.herr, sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
+        *S.herr = 0;
+        NR_CHECK(hipHostGetDevicePointer((void**)&S.derr, S.herr, 0));
+    }
+    NR_CHECK(hipMemcpyAsync(S.off, F.foff, ((size_t)ntiles + 1) * sizeof(u32), hipMemcpyDeviceToDevice, sa));
+    if (items) NR_CHECK(hipMemcpyAsync(S.items, F.fitems, (size_t)items * sizeof(uint4), hipMemcpyDeviceToDevice, sa));
+    NR_CHECK(hipMemcpyAsync(S.dplan, F.dplan, 4 * sizeof(u32), hipMemcpyDeviceToDevice, sa));
+    NR_CHECK(hipEventRecord(S.ready, sa));
+    NR_CHECK(hipEventRecord(F.evVis, sa));   // the set is rewritten only after the copies
+    F.visRecorded = true;
+    S.valid = true;
+    S.tbUid = tb->uid;
+    S.key = key;
+    S.pairs = pairs; S.nitems = items; S.heavy = heavy; S.split = split; S.n = n;
+    S.waitReady = true;
+}
+
+static bool sched_matches(const TriScratch& sc, const TriangleBuffer* tb, const BinKey& key) {
+    return warm_on(sc) && tb && sc.sched.valid && sc.sched.tbUid == tb->uid && !sc.capOverride &&
+           memcmp(&sc.sched.key, &key, sizeof key) == 0;
+}
+
+// A warm batch: one binning kernel into the schedule's ranges (binning set
+// `si`: cursors and pair list), then k_vis over the schedule's items.
+static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinParams& bp) {
+    TriScratch& sc = ctx->tri;
+    auto& S = sc.sched;
+    hipStream_t sa = ctx->stream;
+    hipStream_t sb = warm_inline() ? sa : nr_bin_stream_for(ctx->device);
+    const int ntiles = fp.tiles_x * fp.tiles_y;
+    const int si = sc.fnext;
+    sc.fnext = (sc.fnext + 1) % bin_sets();
+    TriScratch::FreeSet& F = sc.fset[si];
+    if (!F.evBin) { F.evBin = sync_event(); F.evVis = sync_event(); }
+    const size_t tneed = std::max<size_t>((size_t)ntiles + 1, TILE_ARR);
+    const bool grow = F.ftile_cap < tneed || !F.fcnt || F.flist_cap < std::max<size_t>(S.pairs, 1) ||
+                      sc.kslot_cap < std::max<size_t>(S.split, 1) * (TH * TW) || sc.fdone_cap < (size_t)ntiles + 1;
+    if (grow) {   // (first use of a set, or a larger schedule: rare)
+        NR_CHECK(hipStreamSynchronize(sa));
+        NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
+        u32* tb3[3] = {F.fcnt, F.foff, F.fcur};
+        const size_t oldcap = F.ftile_cap;
+        if (!grow_set(tb3, &F.ftile_cap, tneed)) return false;
+        F.fcnt = tb3[0]; F.foff = tb3[1]; F.fcur = tb3[2];
+        if (F.ftile_cap != oldcap) {
+            NR_CHECK(hipMemsetAsync(F.fcnt, 0, F.ftile_cap * sizeof(u32), sa));
+            F.curClean = false;
+        }
+        u32* lb[1] = {F.flist};
+        if (!grow_set(lb, &F.flist_cap, std::max<size_t>(S.pairs, 1))) return false;
+        F.flist = lb[0];
+        u64* kb[1] = {sc.kslot};
+        if (!grow_set(kb, &sc.kslot_cap, std::max<size_t>(S.split, 1) * (TH * TW))) return false;
+        sc.kslot = kb[0];
+        u32* db[1] = {sc.fdone};
+        const size_t olddone = sc.fdone_cap;
+        if (!grow_set(db, &sc.fdone_cap, (size_t)ntiles + 1)) return false;
+        sc.fdone = db[0];
+        if (sc.fdone_cap != olddone) NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.fdone_cap * sizeof(u32), sa));
+    }
+    if (F.visRecorded && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, F.evVis, 0));
+    if (S.waitReady && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, S.ready, 0));
+    S.waitReady = false;
+    if (!F.curClean) NR_CHECK(hipMemsetAsync(F.fcur, 0, (size_t)ntiles * sizeof(u32), sb));
+    const int hbins = bp.hrows * fp.tiles_x;
+    const bool ldsh = 2 * hbins <= LDS_HIST_MAX;
+    const int gb = (int)((bp.src.n + 256 * TPT - 1) / (256 * TPT));
+    hipEvent_t e0, e1;
+    nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
+    const bool xs = ext_stop() && sb != sa && !e1;
+    hipEvent_t binStop = xs ? F.evBin : nullptr;
+    if (ldsh) hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(gb), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
+                                    binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr);
+    else hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(gb), dim3(256), 0, sb, nullptr, binStop, 0, bp, (const u32*)S.off,
+                               F.fcur, F.flist, S.derr);
+    NR_CHECK(hipGetLastError());
+    nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
+    if (sb != sa) {
+        if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
+        NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
+    }
+    // this batch's totals pick the k_vis variant (launch_vis)
+    sc.lastN = S.n; sc.lastPairs = S.pairs; sc.lastHeavy = S.heavy; sc.lastItems = S.nitems; sc.lastSplit = S.split;
+    const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
+    bool visDone = false;
+    if (S.nitems > 0) {
+        nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
+        const bool vs = ext_stop() && !e1;
+        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, S.dplan, F.fcur}, std::min<u32>(S.nitems, 8192), sa,
+                       vs ? F.evVis : nullptr, owned_share_large(fp.period, fp.mask, bp.src.n), zmode,
+                       fp.src.gouraud != 0);
+        NR_CHECK(hipGetLastError());
+        nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+        visDone = vs;
+        F.curClean = true;
+    } else {
+        F.curClean = false;
+    }
+    if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
+    F.visRecorded = true;
+    return true;
 }
 
 }  // namespace
@@ -1729,6 +1978,17 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         sc.lastItems = tb->knownItems;
         sc.lastSplit = tb->knownSplit;
     }
+    // warm: the schedule kept from this buffer's last validated binning under this key
+    if (!ordered && !exact && sched_matches(sc, tb, key)) {
+        if (sc.sched.herr && *(volatile u32*)sc.sched.herr)
+            nr_set_error_msg("triangle batch: a warm binning found a tile over its kept range");
+        if (warm_enqueue(ctx, fp, bp)) {
+            ctx->lastPath = 1;
+            ++sc.warmBatches;
+            finish_batch(ctx, fp);
+        }
+        return;
+    }
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % bin_sets();
     u32 seq = 0;
@@ -1760,9 +2020,18 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         draw_ordered_sorted(ctx, src, fp, bp);
         return;
     }
+    sc.fset[si].curClean = false;   // (its cursors now hold this batch's counts)
+    const int ntiles = fp.tiles_x * fp.tiles_y;
     if (exact) {
-        if (!ordered) record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems, sc.lastSplit);
-    } else if (!known) {
+        if (!ordered) {
+            record_known(tb, key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems, sc.lastSplit);
+            sched_capture(ctx, sc.fset[si], key, tb, ntiles, (u32)sc.lastPairs, sc.lastItems, sc.lastHeavy,
+                          sc.lastSplit, (u64)src.n);
+        }
+    } else if (known) {
+        sched_capture(ctx, sc.fset[si], key, tb, ntiles, tb->knownPairs, tb->knownItems, tb->knownHeavy,
+                      tb->knownSplit, (u64)src.n);
+    } else {
         PendingBatch* pb = new PendingBatch{src, fp, bp, si, seq, tb, key, ordered};
         ctx->pendingBatch = pb;
     }
@@ -1803,8 +2072,12 @@ void settle(RenderContext* ctx) {
     sc.lastHeavy = plan_val(F, 5);
     sc.lastItems = plan_val(F, 1);
     sc.lastSplit = plan_val(F, 2);
-    if (!pb->ordered)   // exact totals, fitted or not
+    if (!pb->ordered) {   // exact totals, fitted or not
         record_known(pb->tb, pb->key, plan_val(F, 0), plan_val(F, 5), plan_val(F, 1), plan_val(F, 2));
+        if (plan_val(F, 3))   // it fitted: its offsets and items are the buffer's schedule under this key
+            sched_capture(ctx, F, pb->key, pb->tb, pb->fp.tiles_x * pb->fp.tiles_y, plan_val(F, 0), plan_val(F, 1),
+                          plan_val(F, 5), plan_val(F, 2), (u64)pb->src.n);
+    }
     if (!plan_val(F, 3)) {
         // overflow (or, ordered, a tile list too long for the LDS sort): the
         // batch's later kernels did nothing; re-run it exactly on the main

@@ -58,6 +58,20 @@ __global__ __launch_bounds__(GV_RT) void k_gvis_init(const BinParams bp, u64* __
     }
 }
 
+#ifndef NR_GV_EXP
+#define NR_GV_EXP 0   // A/B: 1 plain store instead of the atomic (timing only: wrong results), 2 load-then-atomic
+#endif
+__device__ __forceinline__ void gv_min(u64* a, u64 k) {
+    if (NR_GV_EXP == 1) {
+        *a = k;
+    } else if (NR_GV_EXP == 2) {
+        if (k < __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            __hip_atomic_fetch_min(a, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_fetch_min(a, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // One thread per triangle.  Rows [ceil(ymin), ceil(ymax)) of the screen that
 // the rank owns; per row the exact span [xs, xe) of the even-odd rule
 // (relative to x0 = floor(xmin) - 2, clamped to the screen: a conservative
@@ -91,6 +105,11 @@ __global__ __launch_bounds__(GV_T) void k_gvis_raster(const FrameParams fp, u64*
             if (ceil(xmx) + 2 < 0 || floor(xmn) - 2 > (f64)(fp.W - 1)) live = false;
             x0 = clampd(floor(xmn) - 2, 0.0, (f64)fp.W);
         }
+        if (live && r0 < r1 && fp.period > 1) {   // a sharded frame: any owned tile row in [r0, r1)?
+            bool any = false;
+            for (int ty = r0 / TH; ty <= (r1 - 1) / TH && !any; ++ty) any = owned_row(ty, fp.period, fp.mask);
+            live = any;
+        }
         if (live && r0 < r1) {
             const f64 wlim = (f64)fp.W - x0;
             f64 sl[3];
@@ -112,11 +131,10 @@ __global__ __launch_bounds__(GV_T) void k_gvis_raster(const FrameParams fp, u64*
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
                 for (int lx = xs; lx < xe; lx += 2, X += 2.0) {
                     const u32 za = frag_depth(X, dy, sx[0], e1x, e1y, e2x, e2y, inv, zz0, dz1, dz2);
-                    __hip_atomic_fetch_min(row + lx, ((u64)za << 32) | id1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    gv_min(row + lx, ((u64)za << 32) | id1);
                     if (lx + 1 < xe) {
                         const u32 zb = frag_depth(X + 1.0, dy, sx[0], e1x, e1y, e2x, e2y, inv, zz0, dz1, dz2);
-                        __hip_atomic_fetch_min(row + lx + 1, ((u64)zb << 32) | id1, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+                        gv_min(row + lx + 1, ((u64)zb << 32) | id1);
                     }
                 }
             }
@@ -198,6 +216,40 @@ __global__ __launch_bounds__(GV_RT) void k_gvis_resolve(const FrameParams fp, co
     }
 }
 
+// One thread per pixel of an owned row (consecutive lanes, consecutive
+// pixels: the framebuffer rows are written as contiguous runs).
+template <bool GOURAUD>
+__global__ __launch_bounds__(GV_RT) void k_gvis_resolve1(const FrameParams fp, const BinParams bp,
+                                                         u64* __restrict__ gkey, int reset, u64 next) {
+    const i64 y = owned_pixel_row(bp, (int)blockIdx.y);
+    if (y >= fp.H) return;
+    const i64 x = (i64)blockIdx.x * GV_RT + threadIdx.x;
+    if (x >= fp.W) return;
+    const i64 p = y * fp.W + x;
+    const u64 kv = gkey[p];
+    const u32 id = (u32)kv;
+    store_depth<1>(fp, p, kv);
+    if (!id) {
+        if (fp.pendColor) {
+            const f64 v = fp.pendColorValue;
+            store_colour(fp, p, x, y, v, v, v, v);
+        }
+        return;
+    }
+    NR_DEV_CHECK(id <= (u32)fp.src.n, "gvis_resolve: pixel (%ld, %ld) winner %u of %ld triangles", (long)x, (long)y, id,
+                 (long)fp.src.n);
+    f64 rec[RecLen<GOURAUD>::REC];
+    make_record<GOURAUD>(fp, (i64)id - 1, rec);
+    f64 cr, cg, cb, ca;
+    record_colour<GOURAUD>(rec, x, y, cr, cg, cb, ca);
+    apply_winner(fp, p, cr, cg, cb, ca);
+    store_colour(fp, p, x, y, cr, cg, cb, ca);
+    if (reset) gkey[p] = next;
+}
+#ifndef NR_GV_RES1
+#define NR_GV_RES1 1
+#endif
+
 // NR_GVIS: -1 (unset) automatic, 0 never, 1 every eligible batch.
 int gvis_env() {
     static const int v = [] {
@@ -230,6 +282,14 @@ bool gvis_wanted(const RenderContext* ctx, const TriSrc& src, f64 objMeanArea) {
     const int mode = ctx->tri.gvisMode ? ctx->tri.gvisMode : (gvis_env() < 0 ? 0 : (gvis_env() ? 1 : 2));
     if (mode == 1) return true;
     if (mode == 2) return false;
+    // automatic: off -- measured slower than the tiled k_vis on every
+    // configuration (the global 64-bit atomics run at ~36 G/s);
+    // NR_GVIS_AUTO=1 turns the size rule below on
+    static const bool autoOn = [] {
+        const char* e = getenv("NR_GVIS_AUTO");
+        return e && atoi(e) != 0;
+    }();
+    if (!autoOn) return false;
     if (src.n < gvis_min_tris() || !(objMeanArea >= 0)) return false;
     const f64 det = fabs(ctx->m[0] * ctx->m[3] - ctx->m[2] * ctx->m[1]);
     return objMeanArea * det <= gvis_area();
@@ -271,9 +331,15 @@ void draw_gvis(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, con
     const int reset = fp.pendDepth ? 1 : 0;
     const u64 next = (u64)want << 32;
     nr_timing_begin(ctx, NRK_GV_RESOLVE, &e0, &e1);
-    const dim3 rg((unsigned)((fp.W + GV_RT * GV_Q - 1) / (GV_RT * GV_Q)), orows);
-    if (src.gouraud) hipLaunchKernelGGL(k_gvis_resolve<true>, rg, dim3(GV_RT), 0, s, fp, bp, sc.gkey, reset, next);
-    else hipLaunchKernelGGL(k_gvis_resolve<false>, rg, dim3(GV_RT), 0, s, fp, bp, sc.gkey, reset, next);
+    if (NR_GV_RES1) {
+        const dim3 rg((unsigned)((fp.W + GV_RT - 1) / GV_RT), orows);
+        if (src.gouraud) hipLaunchKernelGGL(k_gvis_resolve1<true>, rg, dim3(GV_RT), 0, s, fp, bp, sc.gkey, reset, next);
+        else hipLaunchKernelGGL(k_gvis_resolve1<false>, rg, dim3(GV_RT), 0, s, fp, bp, sc.gkey, reset, next);
+    } else {
+        const dim3 rg((unsigned)((fp.W + GV_RT * GV_Q - 1) / (GV_RT * GV_Q)), orows);
+        if (src.gouraud) hipLaunchKernelGGL(k_gvis_resolve<true>, rg, dim3(GV_RT), 0, s, fp, bp, sc.gkey, reset, next);
+        else hipLaunchKernelGGL(k_gvis_resolve<false>, rg, dim3(GV_RT), 0, s, fp, bp, sc.gkey, reset, next);
+    }
     NR_CHECK(hipGetLastError());
     nr_timing_end(ctx, NRK_GV_RESOLVE, e0, e1);
     sc.gkeyState = reset ? 1 : 0;

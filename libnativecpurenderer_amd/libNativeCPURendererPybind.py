@@ -432,6 +432,15 @@ class RenderContext:
         visibility buffer for small triangles), 1 always, 2 never (tiled)."""
         lib.SetFrameVisRaster(self._ptr, int(mode))
 
+    def set_warm_binning(self, mode: int):
+        """A TriangleBuffer drawn again under the binning key of its last
+        validated draw bins in one pass into the kept tile ranges: 0 automatic
+        (on), 1 on, 2 off (every draw counts, plans and emits)."""
+        lib.SetWarmBinning(self._ptr, int(mode))
+
+    def warm_batch_count(self) -> int:
+        return lib.GetWarmBatchCount(self._ptr)
+
     def set_force_ordered_raster(self, on: bool = True):
         lib.SetForceOrderedRaster(self._ptr, on)
 

@@ -90,12 +90,12 @@ def test_vis_variants_match_oracle(gpu, oracle, mode):
 
 
 def test_c3_gouraud_depth_4k(gpu, gpu_frame, gpu_tiled, oracle):
-    """C3 at full size on both order-free rasterisers (the whole-frame
-    visibility buffer the automatic choice takes for it, and the tiled k_vis)
-    against one oracle frame."""
+    """C3 at full size on both order-free rasterisers (the tiled k_vis the
+    automatic choice takes, and the whole-frame visibility buffer) against one
+    oracle frame."""
     xy, z, c = scenes.sphere_mesh(3840, 2160, 500, 1000)
     o, _ = _tri_frame(oracle, 3840, 2160, xy, z, c)
-    for fac, path in ((gpu, "order-free-frame"), (gpu_frame, "order-free-frame"), (gpu_tiled, "order-free")):
+    for fac, path in ((gpu, "order-free"), (gpu_frame, "order-free-frame"), (gpu_tiled, "order-free")):
         g, ctx = _tri_frame(fac, 3840, 2160, xy, z, c)
         assert ctx.last_raster_path() == path
         assert_same(g, o, "C3 " + path)
@@ -915,3 +915,54 @@ def test_split_dense_tiles_match_oracle(gpu, oracle, limits):
                     ctx.draw_triangles(xy[::3] + 0.5, cc[::3], z=z[::3] * 0.5)   # a second batch over the first
                     outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
                 assert_same(outs[0], outs[1], f"split {limits} depth={depth} write={write} alpha={alpha} g={gouraud}")
+
+
+def _warm_frames(fac, W, H, parts, warm):
+    """A TriangleBuffer (GPU; the same arrays on the oracle) drawn frame after
+    frame: repeats under one binning key bin warm (one pass into the kept tile
+    ranges), a transform change or a different buffer bins cold again and
+    re-captures, a return to the first key is warm again.  The mesh has dense
+    tiles (split work items) and empty ones."""
+    mesh, blob = parts
+    ctx = fac.context(W, H, False)
+    if warm is not None:
+        ctx.set_warm_binning(warm)
+    bufs = None
+    if fac.name == "gpu":
+        from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+        bufs = [R.TriangleBuffer(p[0], p[2], z=p[1], gouraud=True) for p in parts]
+    outs = []
+    for which, xf in [(0, 0), (0, 0), (0, 0), (0, 1), (0, 1), (0, 0), (1, 0), (1, 0), (0, 0), (0, 0)]:
+        ctx.save_state()
+        if xf:
+            ctx.translate(3.5, -2.25)
+            ctx.scale(1.1, 0.9)
+        ctx.set_color(0.1, 0.1, 0.1, 0.1)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        if bufs is not None:
+            ctx.draw_triangle_buffer(bufs[which])
+        else:
+            p = parts[which]
+            ctx.draw_triangles(p[0], p[2], z=p[1])
+        ctx.restore_state()
+        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+    return outs, (ctx.warm_batch_count() if bufs is not None else None)
+
+
+def test_warm_binning_frames(gpu, oracle):
+    W, H = 640, 400
+    mesh = scenes.sphere_mesh(W, H, 100, 300)
+    xy, z, c = scenes.triangle_soup(4000, 60, 40, 3.0, seed=77, gouraud=True)   # one dense tile: split items
+    blob = (xy + np.array([200.0, 100.0] * 3), z, c)
+    both = (np.concatenate([mesh[0], blob[0]]), np.concatenate([mesh[1], blob[1]]), np.concatenate([mesh[2], blob[2]]))
+    parts = (both, mesh)
+    want, _ = _warm_frames(oracle, W, H, parts, None)
+    got, nwarm = _warm_frames(gpu, W, H, parts, 1)
+    for k, (g, o) in enumerate(zip(got, want)):
+        assert_same(g, o, f"warm frame {k}")
+    assert nwarm >= 4, nwarm   # frames 2, 4, 7 and 9 at least (each after a validated draw under its key)
+    cold, ncold = _warm_frames(gpu, W, H, parts, 2)
+    assert ncold == 0
+    for k, (g, o) in enumerate(zip(cold, want)):
+        assert_same(g, o, f"cold frame {k}")

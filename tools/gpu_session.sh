@@ -7,7 +7,7 @@
 #   bench[:ARGS]    python bench.py ARGS  (ARGS: comma-separated, e.g. bench:--config,c2,--steps,20)
 #   trace[:ARGS]    rocprofv3 --kernel-trace --hip-runtime-trace of bench.py ARGS (+ timeline.py)
 #   stats[:ARGS]    rocprofv3 --kernel-trace --stats of bench.py ARGS
-#   ab:ENV1/ENV2/.. bench lines under each environment (ENVk = A=1+B=2), BENCH_ARGS env for the bench flags
+#   ab:ENV1%ENV2%.. bench lines under each environment (ENVk = A=1+B=2), twice, interleaved; BENCH_ARGS env for the bench flags
 #   py:SCRIPT,ARGS  python SCRIPT ARGS
 # Outputs: gpurun_out/$TAG/<step index>_<name>.{log,json}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -43,7 +43,7 @@ for step in "$@"; do
            [ -n "$kt" ] && python3 tools/timeline.py "$kt" 4 > "$OUT/$(printf %02d $i)_timeline.txt" 2>&1 ;;
     stats) d="$OUT/stats$i"
            run stats 600 rocprofv3 --kernel-trace --stats -d "$d" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra "${A[@]}" ;;
-    ab)    IFS='/' read -r -a ENVS <<< "$arg"
+    ab)    IFS='%' read -r -a ENVS <<< "$arg"
            for e in "${ENVS[@]}" "${ENVS[@]}"; do
              run "ab_${e//[^A-Za-z0-9_=]/_}" 300 env ${e//+/ } python bench.py --no-cpu-baseline --no-extra --steps ${STEPS:-100} --warmup 10 $BENCH_ARGS
            done ;;
