@@ -69,7 +69,8 @@ struct TriScratch {
         hipEvent_t evBin = nullptr;         // binning done (binning stream)
         hipEvent_t evVis = nullptr;         // k_vis done reading the set (main stream)
         bool visRecorded = false;
-        bool curClean = false;              // fcur all zero (a warm batch's k_vis re-zeroed it; a cold one leaves counts)
+        u64 curGen = 0;                     // fcur = curEpoch x the counts of schedule curGen (0: unknown)
+        u32 curEpoch = 0;
     } fset[3];
     int fnext = 0;                          // set of the next batch
     u32* fdone = nullptr; size_t fdone_cap = 0;   // split-tile slice counters (k_vis only)
@@ -105,6 +106,7 @@ struct TriScratch {
         u32* dplan = nullptr;                            // the plan's device totals {pairs, items, slices, fits}
         u32 pairs = 0, nitems = 0, heavy = 0, split = 0;
         u64 n = 0;
+        u64 gen = 0;                                     // process-unique generation of this schedule
         hipEvent_t ready = nullptr;                      // the copies above are done (main stream)
         bool waitReady = false;                          // the next warm binning on the binning stream waits for it
         u32* herr = nullptr; u32* derr = nullptr;        // host-mapped: a warm binning found a tile over its range

@@ -659,10 +659,13 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 // former count.  (A tile found over its range -- not possible -- sets *err and
 // its excess pairs are dropped.)  LDSH: hist (next slot) and hlim (range end)
 // per owned tile in LDS.
+// The set's pair cursors are not reset between warm batches: the epoch-th
+// warm batch of one schedule on this set finds cur[t] = epoch * count(t) and
+// takes slots from there (cursor - epoch * count, count = off[t + 1] - off[t]).
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32* __restrict__ off,
                                                   u32* __restrict__ cur, u32* __restrict__ list,
-                                                  u32* __restrict__ err) {
+                                                  u32* __restrict__ err, u32 epoch) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
     const i64 base = (i64)blockIdx.x * 256 * TPT;
@@ -704,10 +707,12 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
             if (h) {
                 const int r = b / bp.tiles_x;
                 const int tile = owned_row_of(bp, r) * bp.tiles_x + (b - r * bp.tiles_x);
-                const u32 start = off[tile] + atomicAdd(&cur[tile], h), end = off[tile + 1];
-                hist[b] = start;
+                const u32 beg = off[tile], end = off[tile + 1];
+                const u32 start = beg + atomicAdd(&cur[tile], h) - epoch * (end - beg);
+                const bool bad = start < beg || start + h > end;
+                hist[b] = bad ? end : start;   // (bad: every slot of this range fails slot < end)
                 hlim[b] = end;
-                if (start + h > end) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (bad) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         __syncthreads();
@@ -728,9 +733,13 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
                     slot = atomicAdd(&hist[hrow + tx], 1u);
                     end = hlim[hrow + tx];
                 } else {
-                    slot = off[hrow + tx] + atomicAdd(&cur[hrow + tx], 1u);
+                    const u32 beg = off[hrow + tx];
                     end = off[hrow + tx + 1];
-                    if (slot >= end) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    slot = beg + atomicAdd(&cur[hrow + tx], 1u) - epoch * (end - beg);
+                    if (slot < beg || slot >= end) {
+                        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        slot = end;
+                    }
                 }
                 if (slot < end) list[slot] = (u32)t;
             }
@@ -1055,7 +1064,7 @@ template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT, int WPE = NR_V
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ kslot, u32* __restrict__ done,
-                                             const u32* __restrict__ plan, u32* __restrict__ zcur) {
+                                             const u32* __restrict__ plan) {
     constexpr bool DEPTH = ZMODE != 0;
     constexpr int NWV = NT / 64;   // waves per workgroup
     // tile keys, rows padded to KS = 65 entries: lanes working on different
@@ -1095,10 +1104,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (le - ls >= (u32)NR_HEAVY_PRIO) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(NR_VIS_BASE_PRIO);
 #endif
-        // warm binning (zcur): the tile's pair cursor goes back to zero for the
-        // binning that next uses this set (every owned tile has an item; a
-        // tile's first slice does it: the binning that counted is done)
-        if (zcur && tid == 0 && (d.w >> 16) == 0) zcur[tile] = 0;
         const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
@@ -1379,13 +1384,11 @@ static bool vis_wpe3(bool big) {
 }
 
 // The k_vis inputs of one batch: its work items, pair list and plan totals
-// (a binning set's, or the warm schedule's), and the pair cursors a warm
-// batch's k_vis re-zeroes (null otherwise).
+// (a binning set's, or the warm schedule's).
 struct VisArgs {
     const uint4* items;
     const u32* list;
     const u32* plan;
-    u32* zcur;
 };
 
 template <int Z, bool C, bool G>
@@ -1400,7 +1403,7 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
     const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wide_heavy();
 #define NR_VIS(CO, NTT, ...)                                                                                       \
     hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, nullptr, stop, 0, fp, va.items,  \
-                          va.list, sc.kslot, sc.fdone, va.plan, va.zcur)
+                          va.list, sc.kslot, sc.fdone, va.plan)
     if (wide) {
         if (coop) NR_VIS(1, 2 * VWG, false, G, true, 2 * VWG);
         else NR_VIS(0, 2 * VWG, false, G, false, 2 * VWG);
@@ -1769,7 +1772,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         const bool vs = ext_stop() && !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
         const bool largeShare = owned_share_large(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
-        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, nullptr}, grid, sa, st, largeShare, zmode, g);
+        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan}, grid, sa, st, largeShare, zmode, g);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
@@ -1836,6 +1839,8 @@ static void sched_capture(RenderContext* ctx, TriScratch::FreeSet& F, const BinK
     S.tbUid = tb->uid;
     S.key = key;
     S.pairs = pairs; S.nitems = items; S.heavy = heavy; S.split = split; S.n = n;
+    static u64 g_gen = 0;
+    S.gen = ++g_gen;
     S.waitReady = true;
 }
 
@@ -1868,7 +1873,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         F.fcnt = tb3[0]; F.foff = tb3[1]; F.fcur = tb3[2];
         if (F.ftile_cap != oldcap) {
             NR_CHECK(hipMemsetAsync(F.fcnt, 0, F.ftile_cap * sizeof(u32), sa));
-            F.curClean = false;
+            F.curGen = 0;
         }
         u32* lb[1] = {F.flist};
         if (!grow_set(lb, &F.flist_cap, std::max<size_t>(S.pairs, 1))) return false;
@@ -1885,7 +1890,13 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (F.visRecorded && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, F.evVis, 0));
     if (S.waitReady && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, S.ready, 0));
     S.waitReady = false;
-    if (!F.curClean) NR_CHECK(hipMemsetAsync(F.fcur, 0, (size_t)ntiles * sizeof(u32), sb));
+    // cursors: epoch e of this schedule on this set (k_bin_warm); zeroed for a
+    // new schedule, after a cold batch on the set, or before they could wrap
+    if (F.curGen != S.gen || (u64)(F.curEpoch + 1) * std::max<u32>(S.pairs, 1) >= 0xF0000000ull) {
+        NR_CHECK(hipMemsetAsync(F.fcur, 0, (size_t)ntiles * sizeof(u32), sb));
+        F.curGen = S.gen;
+        F.curEpoch = 0;
+    }
     const int hbins = bp.hrows * fp.tiles_x;
     const bool ldsh = 2 * hbins <= LDS_HIST_MAX;
     const int gb = (int)((bp.src.n + 256 * TPT - 1) / (256 * TPT));
@@ -1893,10 +1904,11 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
     const bool xs = ext_stop() && sb != sa && !e1;
     hipEvent_t binStop = xs ? F.evBin : nullptr;
+    const u32 epoch = F.curEpoch++;
     if (ldsh) hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(gb), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
-                                    binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr);
+                                    binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr, epoch);
     else hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(gb), dim3(256), 0, sb, nullptr, binStop, 0, bp, (const u32*)S.off,
-                               F.fcur, F.flist, S.derr);
+                               F.fcur, F.flist, S.derr, epoch);
     NR_CHECK(hipGetLastError());
     nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
     if (sb != sa) {
@@ -1910,15 +1922,12 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (S.nitems > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = ext_stop() && !e1;
-        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, S.dplan, F.fcur}, std::min<u32>(S.nitems, 8192), sa,
+        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, S.dplan}, std::min<u32>(S.nitems, 8192), sa,
                        vs ? F.evVis : nullptr, owned_share_large(fp.period, fp.mask, bp.src.n), zmode,
                        fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
-        F.curClean = true;
-    } else {
-        F.curClean = false;
     }
     if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
     F.visRecorded = true;
@@ -2020,7 +2029,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         draw_ordered_sorted(ctx, src, fp, bp);
         return;
     }
-    sc.fset[si].curClean = false;   // (its cursors now hold this batch's counts)
+    sc.fset[si].curGen = 0;   // (its cursors now hold this batch's counts)
     const int ntiles = fp.tiles_x * fp.tiles_y;
     if (exact) {
         if (!ordered) {
