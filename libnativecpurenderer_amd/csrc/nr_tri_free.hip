@@ -2021,6 +2021,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         if (q == hipErrorNotReady) (void)hipGetLastError();   // an answer, not a failure
         else if (q != hipSuccess) NR_CHECK(q);                 // a real asynchronous error: latch it
     }
+    sc.fset[si].curGen = 0;   // (its cursors will hold this batch's counts)
     const int r = free_enqueue(ctx, src, fp, bp, exact, si, pipeOn && tb != nullptr && !exact && !idle, &seq,
                                known ? tb->knownPairs : 0, known ? tb->knownItems : 0, idle, known ? tb->knownSplit : 0,
                                ordered);
@@ -2029,7 +2030,6 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         draw_ordered_sorted(ctx, src, fp, bp);
         return;
     }
-    sc.fset[si].curGen = 0;   // (its cursors now hold this batch's counts)
     const int ntiles = fp.tiles_x * fp.tiles_y;
     if (exact) {
         if (!ordered) {
