@@ -209,7 +209,14 @@ struct TriangleBuffer {
     u32 knownPairs = 0, knownHeavy = 0, knownItems = 0, knownSplit = 0;
     f64 meanArea = -1;    // mean |signed area| of the triangles in user space (computed at upload)
     u64 uid = 0;          // process-unique id (a context's warm schedule names its buffer by it)
+    // per cluster of CLUSTER consecutive triangles (one wave of the binning
+    // kernels): its user-space bounding box {xmin, ymin, xmax, ymax} (NaN when
+    // a vertex is not finite: never culled), computed at upload -- the warm
+    // binning of a sharded frame skips the clusters that lie outside the
+    // rank's tile rows without loading their triangles
+    f64* cbox = nullptr;
 };
+constexpr int NR_CLUSTER = 64;
 
 // host helpers shared across translation units
 Texture* nr_new_texture(i64 w, i64 h, bool alpha);   // device texels, current device

@@ -9,6 +9,7 @@
 #include "nr_tri.h"
 
 #include <algorithm>
+#include <vector>
 #include <atomic>
 #include <cmath>
 
@@ -89,6 +90,26 @@ f64 host_mean_area(const f64* xy, i64 n) {
         if (a < 1e300) { sum += a; ++cnt; }
     }
     return cnt ? sum / (f64)cnt : -1.0;
+}
+
+// User-space bounding boxes of the NR_CLUSTER-triangle clusters (TriangleBuffer::cbox).
+std::vector<f64> host_cluster_boxes(const f64* xy, i64 n) {
+    const i64 nc = (n + NR_CLUSTER - 1) / NR_CLUSTER;
+    std::vector<f64> cb((size_t)nc * 4);
+    for (i64 c = 0; c < nc; ++c) {
+        f64 x0 = INFINITY, y0 = INFINITY, x1 = -INFINITY, y1 = -INFINITY;
+        bool bad = false;
+        for (i64 t = c * NR_CLUSTER; t < std::min<i64>(n, (c + 1) * NR_CLUSTER); ++t)
+            for (int v = 0; v < 3; ++v) {
+                const f64 x = xy[t * 6 + 2 * v], y = xy[t * 6 + 2 * v + 1];
+                if (!std::isfinite(x) || !std::isfinite(y)) bad = true;
+                x0 = std::min(x0, x); x1 = std::max(x1, x);
+                y0 = std::min(y0, y); y1 = std::max(y1, y);
+            }
+        if (bad) x0 = y0 = x1 = y1 = NAN;
+        cb[c * 4] = x0; cb[c * 4 + 1] = y0; cb[c * 4 + 2] = x1; cb[c * 4 + 3] = y1;
+    }
+    return cb;
 }
 
 Opacity host_opacity(const f64* rgba, i64 n, bool gouraud) {
@@ -237,6 +258,8 @@ TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f
     tb->gouraud = gouraud;
     tb->opaque = n > 0 && host_opacity(rgba, n, gouraud) == OPQ_OPAQUE;
     tb->meanArea = n > 0 ? host_mean_area(xy, n) : -1.0;
+    std::vector<f64> cb;
+    if (n > 0) cb = host_cluster_boxes(xy, n);
     NR_CHECK(hipGetDevice(&tb->device));
     hipStream_t s = nr_stream_for(tb->device);
     const size_t ncol = gouraud ? 12 : 4;
@@ -249,6 +272,8 @@ TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f
             NR_CHECK(hipMalloc(&tb->z, (size_t)n * 3 * sizeof(f64)));
             NR_CHECK(hipMemcpyAsync(tb->z, z, (size_t)n * 3 * sizeof(f64), hipMemcpyHostToDevice, s));
         }
+        NR_CHECK(hipMalloc(&tb->cbox, cb.size() * sizeof(f64)));
+        NR_CHECK(hipMemcpyAsync(tb->cbox, cb.data(), cb.size() * sizeof(f64), hipMemcpyHostToDevice, s));
         NR_CHECK(hipStreamSynchronize(s));
     }
     return tb;
@@ -261,9 +286,11 @@ void DestroyTriangleBuffer(TriangleBuffer* tb) {
     nr_settle_all();
     NR_CHECK(hipSetDevice(tb->device));
     NR_CHECK(hipStreamSynchronize(nr_stream_for(tb->device)));
+    NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(tb->device)));
     if (tb->xy) NR_CHECK(hipFree(tb->xy));
     if (tb->z) NR_CHECK(hipFree(tb->z));
     if (tb->rgba) NR_CHECK(hipFree(tb->rgba));
+    if (tb->cbox) NR_CHECK(hipFree(tb->cbox));
     delete tb;
 }
 

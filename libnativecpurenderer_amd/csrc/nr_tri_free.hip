@@ -662,20 +662,53 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 // The set's pair cursors are not reset between warm batches: the epoch-th
 // warm batch of one schedule on this set finds cur[t] = epoch * count(t) and
 // takes slots from there (cursor - epoch * count, count = off[t + 1] - off[t]).
+// Can a cluster (user-space box {xmin, ymin, xmax, ymax}, TriangleBuffer::cbox)
+// put a pair into an owned tile?  Its corners' screen positions bound every
+// vertex's (the affine map's rounded products and sums are monotone in x and
+// y), so a triangle's rows [ceil(ymin), ceil(ymax)) lie in the corners' row
+// range (one row of margin each side); non-finite boxes are never culled.
+__device__ __forceinline__ bool cluster_may_touch(const BinParams& bp, const f64* box) {
+    f64 y0 = INFINITY, y1 = -INFINITY, x0 = INFINITY, x1 = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        f64 sx, sy;
+        nr_xform(bp.m, box[(c & 1) ? 2 : 0], box[(c & 2) ? 3 : 1], sx, sy);
+        if (!isfinite(sx) || !isfinite(sy)) return true;
+        y0 = fmin(y0, sy); y1 = fmax(y1, sy); x0 = fmin(x0, sx); x1 = fmax(x1, sx);
+    }
+    if (x1 < -4.0 || x0 > (f64)bp.W + 4.0) return false;
+    const f64 r0 = fmax(ceil(y0) - 1.0, 0.0), r1 = fmin(ceil(y1) + 1.0, (f64)bp.H);
+    if (!(r0 < r1)) return false;
+    if (bp.period == 1) return true;
+    const int ty0 = (int)r0 / TH, ty1 = ((int)r1 - 1) / TH;
+    for (int ty = ty0; ty <= ty1 && ty < ty0 + 64; ++ty)
+        if (owned_row(ty, bp.period, bp.mask)) return true;
+    return ty1 >= ty0 + 64;
+}
+
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32* __restrict__ off,
                                                   u32* __restrict__ cur, u32* __restrict__ list,
-                                                  u32* __restrict__ err, u32 epoch) {
+                                                  u32* __restrict__ err, u32 epoch, const f64* __restrict__ cbox) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
     const i64 base = (i64)blockIdx.x * 256 * TPT;
     const int hbins = bp.hrows * bp.tiles_x;
     u32* hlim = hist + hbins;
+    // this wave's cluster of each of its TPT triangle groups (NR_CLUSTER == 64:
+    // one wave, so the test and the skip are wave-uniform)
+    static_assert(NR_CLUSTER == 64, "a cluster is one wave's triangles");
+    bool cl[TPT];
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const i64 c = (base + k * 256) / NR_CLUSTER + __builtin_amdgcn_readfirstlane(tid >> 6);
+        cl[k] = !cbox || c * NR_CLUSTER >= bp.src.n || cluster_may_touch(bp, cbox + c * 4);
+    }
     f64 pxy[TPT][6];
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
-        if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
+        if (cl[k] && t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
     }
     if (LDSH) {
         for (int b = tid; b < hbins; b += 256) hist[b] = 0;
@@ -686,7 +719,7 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
         rk[k] = NO_RECT;
-        if (t >= bp.src.n) continue;
+        if (t >= bp.src.n || !cl[k]) continue;
         f64 sx[3], sy[3];
 #pragma unroll
         for (int v = 0; v < 3; ++v) nr_xform(bp.m, pxy[k][2 * v], pxy[k][2 * v + 1], sx[v], sy[v]);
@@ -1851,7 +1884,7 @@ static bool sched_matches(const TriScratch& sc, const TriangleBuffer* tb, const 
 
 // A warm batch: one binning kernel into the schedule's ranges (binning set
 // `si`: cursors and pair list), then k_vis over the schedule's items.
-static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinParams& bp) {
+static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinParams& bp, const f64* tbCbox) {
     TriScratch& sc = ctx->tri;
     auto& S = sc.sched;
     hipStream_t sa = ctx->stream;
@@ -1905,10 +1938,16 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const bool xs = ext_stop() && sb != sa && !e1;
     hipEvent_t binStop = xs ? F.evBin : nullptr;
     const u32 epoch = F.curEpoch++;
+    // cluster culling of the rank's tile rows (NR_CLUSTER_CULL=0: off, A/B)
+    static const bool cullOn = [] {
+        const char* e = getenv("NR_CLUSTER_CULL");
+        return e ? atoi(e) != 0 : true;
+    }();
+    const f64* cbox = cullOn ? tbCbox : nullptr;
     if (ldsh) hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(gb), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
-                                    binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr, epoch);
+                                    binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr, epoch, cbox);
     else hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(gb), dim3(256), 0, sb, nullptr, binStop, 0, bp, (const u32*)S.off,
-                               F.fcur, F.flist, S.derr, epoch);
+                               F.fcur, F.flist, S.derr, epoch, cbox);
     NR_CHECK(hipGetLastError());
     nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
     if (sb != sa) {
@@ -1991,7 +2030,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     if (!ordered && !exact && sched_matches(sc, tb, key)) {
         if (sc.sched.herr && *(volatile u32*)sc.sched.herr)
             nr_set_error_msg("triangle batch: a warm binning found a tile over its kept range");
-        if (warm_enqueue(ctx, fp, bp)) {
+        if (warm_enqueue(ctx, fp, bp, tb->cbox)) {
             ctx->lastPath = 1;
             ++sc.warmBatches;
             finish_batch(ctx, fp);

@@ -44,8 +44,10 @@ for step in "$@"; do
     stats) d="$OUT/stats$i"
            run stats 600 rocprofv3 --kernel-trace --stats -d "$d" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra "${A[@]}" ;;
     ab)    IFS='%' read -r -a ENVS <<< "$arg"
+           rep=0
            for e in "${ENVS[@]}" "${ENVS[@]}"; do
-             run "ab_${e//[^A-Za-z0-9_=]/_}" 300 env ${e//+/ } python bench.py --no-cpu-baseline --no-extra --steps ${STEPS:-100} --warmup 10 $BENCH_ARGS
+             rep=$((rep + 1))
+             run "ab$(printf %02d $rep)_${e//[^A-Za-z0-9_=]/_}" 300 env ${e//+/ } python bench.py --no-cpu-baseline --no-extra --steps ${STEPS:-100} --warmup 10 $BENCH_ARGS
            done ;;
     py)    run "py_$(basename "${A[0]}" .py)" 600 python "${A[@]}" ;;
     *) echo "unknown step $step"; exit 2 ;;
