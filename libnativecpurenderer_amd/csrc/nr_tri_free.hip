@@ -1079,6 +1079,28 @@ constexpr f64 COOP_PAIRS = 2.0;
 #endif
 constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 
+// Per-work-item clocks of k_vis (a build with -DNR_PROBE=1 only: tools/exp/probe.so,
+// tools/exp/probe_items.py): item, {tile, list begin, end, slices}, start and end
+// (s_memrealtime, 100 MHz), workgroup size.
+#ifndef NR_PROBE
+#define NR_PROBE 0
+#endif
+#if NR_PROBE
+constexpr int PROBE_MAX = 65536;
+__device__ unsigned long long nr_probe_buf[PROBE_MAX * 4];
+__device__ unsigned int nr_probe_n;
+__device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, int nt) {
+    const u32 k = atomicAdd(&nr_probe_n, 1u);
+    if (k >= PROBE_MAX) return;
+    unsigned long long* e = nr_probe_buf + (size_t)k * 4;
+    e[0] = (u64)item | ((u64)nt << 32);
+    e[1] = (u64)d.x | ((u64)d.w << 32);
+    e[2] = (u64)d.y | ((u64)d.z << 32);
+    e[3] = 0;
+    __hip_atomic_store(&e[3], (t1 - t0) | (t0 << 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
+
 // One workgroup per work item (tile, slice of <= SLICE triangles).  The 4
 // waves share only the tile's 2048 LDS keys; each wave independently walks
 // 64-triangle chunks of the slice (chunk c goes to wave c % 4) with no
@@ -1121,9 +1143,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // grid-stride over the work items (the grid is sized from a capacity
     // bound, not from the item count, so no host sync is needed)
     uint4 dnext = blockIdx.x < nitems ? items[blockIdx.x] : make_uint4(0, 0, 0, 0);
+#if NR_PROBE
+    u64 pr_t0 = 0;
+    u32 pr_item = ~0u;
+    uint4 pr_d = make_uint4(0, 0, 0, 0);
+#endif
     for (u32 item = blockIdx.x; item < nitems; item += gridDim.x) {
         const uint4 d = dnext;
         if (item + gridDim.x < nitems) dnext = items[item + gridDim.x];
+#if NR_PROBE
+        if (tid == 0) {
+            const u64 now = __builtin_amdgcn_s_memrealtime();
+            if (pr_item != ~0u) probe_item(pr_item, pr_d, pr_t0, now, NT);
+            pr_t0 = now; pr_item = item; pr_d = d;
+        }
+#endif
         __syncthreads();
         const int tile = (int)d.x;
         const u32 ls = d.y, le = d.z;
@@ -1378,6 +1412,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         __syncthreads();
         shade_tile<ZMODE, GOURAUD, NT, HS>(fp, x0, y0, wlim, hlim, key, lds, nU);
     }   // work items
+#if NR_PROBE
+    if (tid == 0 && pr_item != ~0u) probe_item(pr_item, pr_d, pr_t0, __builtin_amdgcn_s_memrealtime(), NT);
+#endif
     if (COUNT) {
         __syncthreads();
         atomicAdd(&sFrag, myFrags);
@@ -2141,3 +2178,22 @@ void settle(RenderContext* ctx) {
 }
 
 }  // namespace nrtri
+
+#if NR_PROBE
+extern "C" {
+// probe build only: clear / read the k_vis per-item clocks (4 u64 per item)
+void NrProbeReset() {
+    const unsigned int z = 0;
+    NR_CHECK(hipDeviceSynchronize());
+    NR_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(nrtri::nr_probe_n), &z, sizeof z));
+}
+i64 NrProbeRead(unsigned long long* out, i64 maxItems) {
+    unsigned int n = 0;
+    NR_CHECK(hipDeviceSynchronize());
+    NR_CHECK(hipMemcpyFromSymbol(&n, HIP_SYMBOL(nrtri::nr_probe_n), sizeof n));
+    const i64 m = std::min<i64>(std::min<i64>((i64)n, maxItems), nrtri::PROBE_MAX);
+    NR_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(nrtri::nr_probe_buf), (size_t)m * 4 * sizeof(unsigned long long)));
+    return m;
+}
+}
+#endif
