@@ -180,26 +180,34 @@ __device__ __forceinline__ u32 wave_scan(u32 v, int) {
 
 constexpr int PLAN_T = 1024, PLAN_W = PLAN_T / 64;
 constexpr u32 HEAVY_PAIRS = 256;   // a dense tile (for the k_vis workgroup-size choice)
-constexpr int PLAN_NB = 12;
-
-// Size class of a tile's work items: 0 empty, 1 + the count's bin (below) for
-// one slice, PLAN_NB - 1 for tiles split over several slices.  Items are
-// laid out largest class first: k_vis workgroups take items in index order,
-// so the long ones start first and the short ones fill the tail (a longest-
-// first schedule).  Results do not depend on the order (order-free raster).
-// One-slice classes are PLAN_NB - 2 equal bins of [1, lim] (NR_CLASS_LIN=0:
+// Size classes of a tile's work items: 0 empty; 1..PLAN_ONE one slice, by
+// the count's bin (below); the PLAN_SPLIT highest for tiles split over
+// several slices, by their slice count (>= 8, 4-7, 2-3).  Items are laid out
+// largest class first: k_vis workgroups take items in index order, so the
+// long ones start first and the short ones fill the tail (a longest-first
+// schedule).  Results do not depend on the order (order-free raster).  The
+// split classes come first, so split items take the indices [0, slices) --
+// their key slots.  The densest tiles' slices first (round 4): their last
+// slice merges the others' keys and shades the tile, the kernel's longest
+// chain (a 16-slice 1080p tile started 62 us into a 98 us raster,
+// tools/exp/probe_items.py).
+// One-slice classes are PLAN_ONE equal bins of [1, lim] (NR_CLASS_LIN=0:
 // octaves, which left a C3 frame's items -- nearly all in [256, 1024] -- in
 // two classes, in tile order within each): C3 -0.8 %, 1M tris at 1080p -1.3 %,
 // C2 -2 % per frame (profiles/r03_c3/ab_class_lin.txt).
+constexpr int PLAN_ONE = 10, PLAN_SPLIT = 3, PLAN_NB = 1 + PLAN_ONE + PLAN_SPLIT;
 #ifndef NR_CLASS_LIN
 #define NR_CLASS_LIN 1
 #endif
-__device__ __forceinline__ int size_class(u32 c, u32 lim) {
-    if (c > lim) return PLAN_NB - 1;
+__device__ __forceinline__ int size_class(u32 c, u32 lim, u32 dsl) {
+    if (c > lim) {
+        const u32 ni = (c + dsl - 1) / dsl;
+        return PLAN_NB - (ni >= 8 ? 1 : ni >= 4 ? 2 : 3);
+    }
     if (c == 0) return 0;
-    if (NR_CLASS_LIN) return 1 + min((int)((float)c * ((float)(PLAN_NB - 2) / (float)(lim + 1))), PLAN_NB - 3);
+    if (NR_CLASS_LIN) return 1 + min((int)((float)c * ((float)PLAN_ONE / (float)(lim + 1))), PLAN_ONE - 1);
     const int l = 31 - __clz(c);
-    return 1 + (l < PLAN_NB - 3 ? l : PLAN_NB - 3);
+    return 1 + (l < PLAN_ONE - 1 ? l : PLAN_ONE - 1);
 }
 
 // Tiles are taken PLAN_T at a time (thread = tile: coalesced), each round a
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         const u32 ni = tile_items(c, owned_row(i / tiles_x, period, mask), lim, dsl);
         b += ni;
         m += ni > 1 ? ni : 0u;
-        if (ni) atomicAdd(&bcnt[size_class(c, lim)], ni);
+        if (ni) atomicAdd(&bcnt[size_class(c, lim, dsl)], ni);
     }
     b = wave_scan(b, lane); m = wave_scan(m, lane);
     if (lane == 63) { sh[1][w] = b; sh[2][w] = m; }
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
         if (i < ntiles) {
             off[i] = ea;
             if (fits && ni) {
-                const u32 eb = atomicAdd(&bcur[size_class(c, lim)], ni);
+                const u32 eb = atomicAdd(&bcur[size_class(c, lim, dsl)], ni);
                 for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c, k, ni);
             }
             cnt[i] = 0;
@@ -353,7 +361,7 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
             const u32 ni = tile_items(c[j], owned_row((i0 + j) / tiles_x, period, mask), lim, dsl);
             b += ni;
             m += ni > 1 ? ni : 0u;
-            if (ni) atomicAdd(&bcnt[size_class(c[j], lim)], ni);
+            if (ni) atomicAdd(&bcnt[size_class(c[j], lim, dsl)], ni);
         }
     }
     b = wave_scan(b, lane); m = wave_scan(m, lane);
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
             off[i] = ea;
             const u32 ni = tile_items(c[j], owned_row(i / tiles_x, period, mask), lim, dsl);
             if (fits && ni) {
-                const u32 eb = atomicAdd(&bcur[size_class(c[j], lim)], ni);
+                const u32 eb = atomicAdd(&bcur[size_class(c[j], lim, dsl)], ni);
                 for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c[j], k, ni);
             }
             cnt[i] = 0;
@@ -481,7 +489,7 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
             const u32 ni = (j < per && i0 + j < ntiles) ? tile_items(c[j], owned_row(ty, period, mask), lim, dsl) : 0u;
             b += ni;
             m += ni > 1 ? ni : 0u;
-            const int cls = size_class(c[j], lim);
+            const int cls = size_class(c[j], lim, dsl);
 #pragma unroll
             for (int k = 0; k < PLAN_NB; ++k) hc[k] += cls == k ? ni : 0u;
             if (++tx == tiles_x) { tx = 0; ++ty; }
@@ -531,7 +539,7 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
             c[j] = ea;
             const int i = i0 + j;
             const u32 ni = (j < per && i < ntiles) ? tile_items(cj, owned_row(ty, period, mask), lim, dsl) : 0u;
-            const int cls = size_class(cj, lim);
+            const int cls = size_class(cj, lim, dsl);
             u32 eb = 0;
 #pragma unroll
             for (int k = 0; k < PLAN_NB; ++k)
@@ -1168,7 +1176,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         // the longest work items (dense tiles' slices) set the kernel's
         // critical path: their waves win the SIMD's issue arbitration over the
         // short items that run beside them
-        if (le - ls >= (u32)NR_HEAVY_PRIO) __builtin_amdgcn_s_setprio(3);
+#ifndef NR_PRIO_SPLIT
+#define NR_PRIO_SPLIT 1   // the slices of split tiles too (their last slice merges and shades: the longest chains)
+#endif
+        if (le - ls >= (u32)NR_HEAVY_PRIO || (NR_PRIO_SPLIT && multi)) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(NR_VIS_BASE_PRIO);
 #endif
         const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
@@ -1393,15 +1404,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 const int p = tid + j * NT;
                 kk[j] = key[(p / TW) * KS + (p & (TW - 1))];
             }
-            for (u32 sl = 0; sl < nsl; ++sl) {
-                if (first + sl == item) continue;
-                const u64* slot = kslot + (size_t)(first + sl) * (TH * TW);
-                u64 v[PR];
+            // MB slots per round, all their loads in flight together (16 keys
+            // per thread): a 16-slice pole tile's merge is 4 latency rounds,
+            // not 16.  This slice's own slot and the padding past the last
+            // slice read slot `first` again: min / max are idempotent.
+            constexpr int MB = PR >= 8 ? 2 : (PR >= 4 ? 4 : 8);
+            for (u32 sl = 0; sl < nsl; sl += MB) {
+                u64 v[MB][PR];
 #pragma unroll
-                for (int j = 0; j < PR; ++j)
-                    v[j] = __hip_atomic_load(slot + tid + j * NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int b = 0; b < MB; ++b) {
+                    const u32 s2 = sl + b < nsl ? sl + b : 0u;
+                    const u64* slot = kslot + (size_t)(first + s2) * (TH * TW);
 #pragma unroll
-                for (int j = 0; j < PR; ++j) kk[j] = ZMODE == 1 ? (v[j] < kk[j] ? v[j] : kk[j]) : (v[j] > kk[j] ? v[j] : kk[j]);
+                    for (int j = 0; j < PR; ++j)
+                        v[b][j] = __hip_atomic_load(slot + tid + j * NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+#pragma unroll
+                for (int b = 0; b < MB; ++b)
+#pragma unroll
+                    for (int j = 0; j < PR; ++j)
+                        kk[j] = ZMODE == 1 ? (v[b][j] < kk[j] ? v[b][j] : kk[j]) : (v[b][j] > kk[j] ? v[b][j] : kk[j]);
             }
 #pragma unroll
             for (int j = 0; j < PR; ++j) {

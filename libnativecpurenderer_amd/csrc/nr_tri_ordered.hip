@@ -337,6 +337,28 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
             // this wave's block
             for (; hm; hm &= hm - 1) {
                 const int k = (int)__builtin_ctzll(hm);
+#ifndef NR_ORD_L0
+#define NR_ORD_L0 0   // A/B: the unit's masks and blend terms read by lane 0 only (LDS bytes / 64), then readfirstlane
+#endif
+#if NR_ORD_L0
+                u64 lm[RPW];
+                f64 om, RA, GA, BA, fA = 0.0;
+                {
+                    ulonglong2 m01 = make_ulonglong2(0, 0), m23 = make_ulonglong2(0, 0);
+                    f64 t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+                    if (lane == 0) {
+                        m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
+                        m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
+                        t0 = S[S_OM][k]; t1 = S[S_RA][k]; t2 = S[S_GA][k]; t3 = S[S_BA][k];
+                        if (RGBA) t4 = S[S_FA][k];
+                    }
+                    lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
+                    lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
+                    auto uf = [](f64 v) { return __longlong_as_double((long long)uniform_u64((u64)__double_as_longlong(v))); };
+                    om = uf(t0); RA = uf(t1); GA = uf(t2); BA = uf(t3);
+                    if (RGBA) fA = uf(t4);
+                }
+#else
                 const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
                 const f64 fA = RGBA ? S[S_FA][k] : 0.0;
                 u64 lm[RPW];
@@ -344,6 +366,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
                 const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
                 lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
                 lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
+#endif
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
                     if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
