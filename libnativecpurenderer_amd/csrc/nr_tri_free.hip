@@ -39,6 +39,35 @@
 namespace nrtri {
 namespace {
 
+// Per-work-item clocks of k_vis (a build with -DNR_PROBE=1 only: tools/exp/probe.so,
+// tools/exp/probe_items.py): item, {tile, list begin, end, slices}, start and end
+// (s_memrealtime, 100 MHz), workgroup size.
+#ifndef NR_PROBE
+#define NR_PROBE 0
+#endif
+#if NR_PROBE
+constexpr int PROBE_MAX = 65536;
+__device__ unsigned long long nr_probe_buf[PROBE_MAX * 8];
+__device__ unsigned int nr_probe_n;
+__shared__ u64 pr_st[8];   // phase stamps of the current item (thread 0): 1 keys set, 2 raster, 3 merge, 4 hash, 5 records
+#define NR_PROBE_STAMP(k) do { if (threadIdx.x == 0) pr_st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, int nt) {
+    const u32 k = atomicAdd(&nr_probe_n, 1u);
+    if (k >= PROBE_MAX) return;
+    unsigned long long* e = nr_probe_buf + (size_t)k * 8;
+    e[0] = (u64)item | ((u64)nt << 32);
+    e[1] = (u64)d.x | ((u64)d.w << 32);
+    e[2] = (u64)d.y | ((u64)d.z << 32);
+    auto rel = [&](int q) { return pr_st[q] >= t0 && pr_st[q] <= t1 ? (pr_st[q] - t0) & 0xFFFF : 0xFFFFull; };
+    e[4] = rel(1) | (rel(2) << 16) | (rel(3) << 32) | (rel(4) << 48);
+    e[5] = rel(5);
+    __hip_atomic_store(&e[3], (t1 - t0) | (t0 << 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = 1; q < 6; ++q) pr_st[q] = 0;
+}
+#else
+#define NR_PROBE_STAMP(k) do { } while (0)
+#endif
+
 #ifndef NR_VWG
 #define NR_VWG 256
 #endif
@@ -953,6 +982,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         if (OVF_Q && !placed) ovf |= 1u << k;
     }
     __syncthreads();   // every key read: the records may overwrite them
+    NR_PROBE_STAMP(4);
     const u32 U = nU < (u32)St::RT ? nU : (u32)St::RT;
 #ifndef NR_REC_Q
 #define NR_REC_Q 2
@@ -971,6 +1001,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
         for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);
     }
     __syncthreads();
+    NR_PROBE_STAMP(5);
 #pragma unroll 1
     for (int k = 0; k < PPT; ++k) {
         const int p = tid + k * NT, lx = p & (TW - 1), ly = p / TW;
@@ -1087,27 +1118,7 @@ constexpr f64 COOP_PAIRS = 2.0;
 #endif
 constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 
-// Per-work-item clocks of k_vis (a build with -DNR_PROBE=1 only: tools/exp/probe.so,
-// tools/exp/probe_items.py): item, {tile, list begin, end, slices}, start and end
-// (s_memrealtime, 100 MHz), workgroup size.
-#ifndef NR_PROBE
-#define NR_PROBE 0
-#endif
-#if NR_PROBE
-constexpr int PROBE_MAX = 65536;
-__device__ unsigned long long nr_probe_buf[PROBE_MAX * 4];
-__device__ unsigned int nr_probe_n;
-__device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, int nt) {
-    const u32 k = atomicAdd(&nr_probe_n, 1u);
-    if (k >= PROBE_MAX) return;
-    unsigned long long* e = nr_probe_buf + (size_t)k * 4;
-    e[0] = (u64)item | ((u64)nt << 32);
-    e[1] = (u64)d.x | ((u64)d.w << 32);
-    e[2] = (u64)d.y | ((u64)d.z << 32);
-    e[3] = 0;
-    __hip_atomic_store(&e[3], (t1 - t0) | (t0 << 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#endif
+
 
 // One workgroup per work item (tile, slice of <= SLICE triangles).  The 4
 // waves share only the tile's 2048 LDS keys; each wave independently walks
@@ -1205,6 +1216,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             if (ZMODE == 2) zin[ly * KS + lx] = z0;
         }
         __syncthreads();
+        NR_PROBE_STAMP(1);
 
         // this wave's chunks: c = wave, wave + NW, ...  One lane per triangle,
         // its setup in registers; the lane walks the triangle's rows in this
@@ -1362,6 +1374,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             }
         }
         __syncthreads();
+        NR_PROBE_STAMP(2);
         if (!multi) {   // the whole list was in this slice: shade now
             if (rlo < rcap)
                 shade_tile<ZMODE, GOURAUD, NT, HS>(fp, x0, y0 + rlo, wlim, rcap - rlo, key + rlo * KS, lds, nU);
@@ -1432,6 +1445,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             }
         }
         __syncthreads();
+        NR_PROBE_STAMP(3);
         shade_tile<ZMODE, GOURAUD, NT, HS>(fp, x0, y0, wlim, hlim, key, lds, nU);
     }   // work items
 #if NR_PROBE
@@ -2203,7 +2217,7 @@ void settle(RenderContext* ctx) {
 
 #if NR_PROBE
 extern "C" {
-// probe build only: clear / read the k_vis per-item clocks (4 u64 per item)
+// probe build only: clear / read the k_vis per-item clocks (8 u64 per item)
 void NrProbeReset() {
     const unsigned int z = 0;
     NR_CHECK(hipDeviceSynchronize());
@@ -2214,7 +2228,7 @@ i64 NrProbeRead(unsigned long long* out, i64 maxItems) {
     NR_CHECK(hipDeviceSynchronize());
     NR_CHECK(hipMemcpyFromSymbol(&n, HIP_SYMBOL(nrtri::nr_probe_n), sizeof n));
     const i64 m = std::min<i64>(std::min<i64>((i64)n, maxItems), nrtri::PROBE_MAX);
-    NR_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(nrtri::nr_probe_buf), (size_t)m * 4 * sizeof(unsigned long long)));
+    NR_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(nrtri::nr_probe_buf), (size_t)m * 8 * sizeof(unsigned long long)));
     return m;
 }
 }

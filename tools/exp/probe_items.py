@@ -44,9 +44,9 @@ ctx.flush()
 lib.NrProbeReset()
 frame()
 ctx.flush()
-out = np.zeros(65536 * 4, np.uint64)
+out = np.zeros(65536 * 8, np.uint64)
 n = lib.NrProbeRead(out.ctypes.data, 65536)
-e = out[: 4 * n].reshape(n, 4)
+e = out[: 8 * n].reshape(n, 8)
 item = (e[:, 0] & 0xFFFFFFFF).astype(np.int64)
 nt = (e[:, 0] >> 32).astype(np.int64)
 tile = (e[:, 1] & 0xFFFFFFFF).astype(np.int64)
@@ -76,3 +76,16 @@ busy = [int(((t0 <= t) & (t1 > t)).sum()) for t in ts]
 print("busy workgroups over the span:", " ".join(str(b) for b in busy))
 starts = np.sort(t0)
 print("item starts at 25/50/75/90/100 %:", " ".join(f"{np.percentile(starts, p):.1f}" for p in (25, 50, 75, 90, 100)))
+
+# phases (thread 0's clock at the barriers): keys set, raster done, merge done (split), hash done, records done, end
+ph = np.stack([((e[:, 4] >> (16 * q)) & 0xFFFF) for q in range(4)] + [e[:, 5] & 0xFFFF], 1).astype(np.float64)
+ph[ph == 0xFFFF] = np.nan
+ph /= 100.0
+names = ["keys", "raster", "merge", "hash", "records"]
+print("phase end times (us after item start), mean over items with pairs; single-slice / split-last:")
+single = (L > 0) & (nsl == 1)
+last = (L > 0) & (nsl > 1) & ~np.isnan(ph[:, 3])
+for lab, m in (("single", single), ("split last", last)):
+    if m.any():
+        cols = [f"{nm} {np.nanmean(ph[m, q]):5.1f}" for q, nm in enumerate(names)]
+        print(f"  {lab:10s} n={m.sum():5d}  " + "  ".join(cols) + f"  end {dur[m].mean():5.1f}")
