@@ -817,6 +817,17 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     }
 }
 
+// threadIdx.x as a value the compiler cannot see through: the per-pixel LDS
+// and global addresses the item phases derive from it are then formed where
+// they are used, inside the item loop, instead of being hoisted to the kernel
+// prologue and kept live (spilled) across the whole raster -- the 4-wave
+// instances' spills were mostly those hoisted addresses.
+__device__ __forceinline__ int opaque_tid() {
+    int t = (int)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // ---- deferred shading --------------------------------------------------
 // A workgroup shades its tile after the raster.  The winners of the tile's
 // pixels are few (a triangle wins ~9 pixels of the C3 mesh), so they are
@@ -883,7 +894,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
     using St = ShadeStage<GOURAUD, HS>;
     constexpr int PPT = TH * TW / NT;
     static_assert(PPT <= 32, "overflow bitmask");
-    const int tid = threadIdx.x;
+    const int tid = opaque_tid();
 #ifndef NR_FLAT_DIRECT
 #define NR_FLAT_DIRECT 1
 #endif
@@ -1120,6 +1131,8 @@ constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 
 
 
+
+
 // One workgroup per work item (tile, slice of <= SLICE triangles).  The 4
 // waves share only the tile's 2048 LDS keys; each wave independently walks
 // 64-triangle chunks of the slice (chunk c goes to wave c % 4) with no
@@ -1178,6 +1191,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
 #endif
         __syncthreads();
+        const int itid = opaque_tid();   // (this item's per-pixel addresses: formed here, not kept live)
         const int tile = (int)d.x;
         const u32 ls = d.y, le = d.z;
         const u32 nsl = d.w & 0xFFFFu;   // slices of the tile (d.w >> 16: this item's slice)
@@ -1199,7 +1213,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
         const int rcap = hlim;   // rows [rlo, rcap) of the tile are rasterised here
         if (ls == le) {   // no triangle: only the pending clears
-            for (int p = tid; p < TH * TW; p += NT) {
+            for (int p = itid; p < TH * TW; p += NT) {
                 const int lx = p & (TW - 1), ly = p / TW;
                 if (lx < wlim && ly < hlim)
                     store_clear<ZMODE>(fp, (y0 + ly) * fp.W + x0 + lx, x0 + lx, y0 + ly);
@@ -1207,7 +1221,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             continue;
         }
 
-        for (int p = tid; p < TH * TW; p += NT) {
+        for (int p = itid; p < TH * TW; p += NT) {
             const int lx = p & (TW - 1), ly = p / TW;
             u32 z0 = 0xFFFFFFFFu;
             if (DEPTH && lx < wlim && ly < hlim)
@@ -1293,39 +1307,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #ifndef NR_SPAN32_WPE3
 #define NR_SPAN32_WPE3 0
 #endif
-            constexpr bool SPAN32 = NR_SPAN32 && (WPE != 3 || NR_SPAN32_WPE3);
-            if (r0 < r1 && !big) {
-                Span32 S32;
-                if (SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);
-#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-                for (int r = r0; r < r1; ++r) {
-                    const f64 y = (f64)(int)(y0 + r);
-                    int xs, xe;
-                    if (!SPAN32) row_span_slopes(sx, sy, sl, y, (f64)x0, (f64)wlim, xs, xe);
-                    else if (!row_span32(S32, r, y, (float)wlim, xs, xe))
-                        row_span_in(sx, sy, y, (f64)x0, (f64)wlim, xs, xe);   // (rare: the exact statement)
-                    if (COUNT) myFrags += (unsigned long long)(xe - xs);
-                    if (xs >= xe) continue;
-                    if (ZMODE == 0) {
-#pragma clang loop vectorize(disable) interleave(disable)
-                        for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * KS + lx], id1);
-                        continue;
-                    }
-                    const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
-                    // two pixels per step: independent chains (ILP) and half the
-                    // divergent trip count for the short spans of sliver triangles
-                    f64 X = (f64)(int)(x0 + xs);   // pixel x as f64, exact (integers < 2^31)
-#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-                    for (int lx = xs; lx < xe; lx += 2, X += 2.0) {
-                        frag_key<ZMODE>(key, zin, r * KS + lx, X, dy, sx[0], e1x, e1y, e2x, e2y, inv, zz0, dz1, dz2,
-                                        id1);
-                        if (lx + 1 < xe)
-                            frag_key<ZMODE>(key, zin, r * KS + lx + 1, X + 1.0, dy, sx[0], e1x, e1y, e2x, e2y, inv,
-                                            zz0, dz1, dz2, id1);
-                    }
-                }
-            }
-            // the wave's large triangles, one at a time, all lanes on each
+#ifndef NR_SPAN32_FLAT
+#define NR_SPAN32_FLAT 0   // flat batches: the f64 spans (the f32 ones cost the flat instances 8-24 B/lane of spills)
+#endif
+            constexpr bool SPAN32 = NR_SPAN32 && (WPE != 3 || NR_SPAN32_WPE3) && (GOURAUD || NR_SPAN32_FLAT) &&
+                                    ZMODE != 2 && !COUNT;
+            // the wave's large triangles first, one at a time, all lanes on each
+            // (the keys are an order-free min / max, so the order of the two
+            // passes is free; this one reads every lane's screen vertices, so
+            // they are dead before the lane raster below)
             for (u64 bm = COOP ? __ballot(big && r0 < r1) : 0ull; bm; bm &= bm - 1) {
                 const int src = (int)__builtin_ctzll(bm);
                 f64 bx[3], by[3], bs[3];
@@ -1372,6 +1362,45 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                     bd1, bd2, bid);
                 }
             }
+            if (r0 < r1 && !big) {
+                Span32 S32;
+                if (SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+                for (int r = r0; r < r1; ++r) {
+                    const f64 y = (f64)(int)(y0 + r);
+                    int xs, xe;
+                    if (!SPAN32) {
+                        row_span_slopes(sx, sy, sl, y, (f64)x0, (f64)wlim, xs, xe);
+                    } else if (!row_span32(S32, r, y, (float)wlim, xs, xe)) {
+                        // (rare: the exact statement.)  The screen vertices are
+                        // formed again from the triangle's positions rather than
+                        // kept live through the row loop: 8 fewer VGPRs there,
+                        // the 4-wave instances' register peak
+                        f64 qx[3], qy[3];
+                        tri_screen(fp.src, fp.m, (i64)id1 - 1, qx, qy);
+                        row_span_in(qx, qy, y, (f64)x0, (f64)wlim, xs, xe);
+                    }
+                    if (COUNT) myFrags += (unsigned long long)(xe - xs);
+                    if (xs >= xe) continue;
+                    if (ZMODE == 0) {
+#pragma clang loop vectorize(disable) interleave(disable)
+                        for (int lx = xs; lx < xe; ++lx) atomicMax(&key[r * KS + lx], id1);
+                        continue;
+                    }
+                    const f64 dy = y - sy[0];   // (f64)j - pts[0][1], as the oracle
+                    // two pixels per step: independent chains (ILP) and half the
+                    // divergent trip count for the short spans of sliver triangles
+                    f64 X = (f64)(int)(x0 + xs);   // pixel x as f64, exact (integers < 2^31)
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+                    for (int lx = xs; lx < xe; lx += 2, X += 2.0) {
+                        frag_key<ZMODE>(key, zin, r * KS + lx, X, dy, sx[0], e1x, e1y, e2x, e2y, inv, zz0, dz1, dz2,
+                                        id1);
+                        if (lx + 1 < xe)
+                            frag_key<ZMODE>(key, zin, r * KS + lx + 1, X + 1.0, dy, sx[0], e1x, e1y, e2x, e2y, inv,
+                                            zz0, dz1, dz2, id1);
+                    }
+                }
+            }
         }
         __syncthreads();
         NR_PROBE_STAMP(2);
@@ -1392,7 +1421,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         // barrier, and the slice counter is a relaxed device atomic.
         {
             u64* const mine = kslot + (size_t)item * (TH * TW);
-            for (int p = tid; p < TH * TW; p += NT)   // (every key: pixels past the frame edge are never shaded)
+            for (int p = itid; p < TH * TW; p += NT)   // (every key: pixels past the frame edge are never shaded)
                 __hip_atomic_store(&mine[p], key[(p / TW) * KS + (p & (TW - 1))], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1414,7 +1443,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             u64 kk[PR];
 #pragma unroll
             for (int j = 0; j < PR; ++j) {
-                const int p = tid + j * NT;
+                const int p = itid + j * NT;
                 kk[j] = key[(p / TW) * KS + (p & (TW - 1))];
             }
             // MB slots per round, all their loads in flight together (16 keys
@@ -1430,7 +1459,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                     const u64* slot = kslot + (size_t)(first + s2) * (TH * TW);
 #pragma unroll
                     for (int j = 0; j < PR; ++j)
-                        v[b][j] = __hip_atomic_load(slot + tid + j * NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        v[b][j] = __hip_atomic_load(slot + itid + j * NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
 #pragma unroll
                 for (int b = 0; b < MB; ++b)
@@ -1440,7 +1469,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             }
 #pragma unroll
             for (int j = 0; j < PR; ++j) {
-                const int p = tid + j * NT;
+                const int p = itid + j * NT;
                 key[(p / TW) * KS + (p & (TW - 1))] = kk[j];
             }
         }
