@@ -1510,12 +1510,17 @@ static u32 wide_heavy() {
 // 0.1609 ms per frame; profiles/r02_c3/ab_wpe3.txt).  Short batches (C2, an
 // 8-way share) keep 4 waves: their rasters are short and occupancy-bound
 // (+15 % at 3).  NR_VIS_WPE3=0 keeps 4 waves everywhere (A/B).
+// Round 4: off by default.  With the per-item addresses no longer hoisted
+// (opaque_tid) the 4-wave instances need no more than 128 VGPRs without
+// spills, and a warm batch bins inline before its raster, so no binning kernel
+// needs the slot the 3-wave instance left free: C3 0.147 -> 0.140 ms per frame
+// at 4 waves (profiles/r04/ab_instances.txt).  NR_VIS_WPE3=1 forces it (A/B).
 static bool vis_wpe3(bool big) {
     static const int v = [] {
         const char* e = getenv("NR_VIS_WPE3");
-        return e ? atoi(e) : -1;
+        return e ? atoi(e) : 0;
     }();
-    return v >= 0 ? v != 0 : big;
+    return v == 2 ? big : v != 0;
 }
 
 // The k_vis inputs of one batch: its work items, pair list and plan totals
