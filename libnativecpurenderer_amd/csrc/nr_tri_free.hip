@@ -735,17 +735,34 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     // this wave's cluster of each of its TPT triangle groups (NR_CLUSTER == 64:
     // one wave, so the test and the skip are wave-uniform)
     static_assert(NR_CLUSTER == 64, "a cluster is one wave's triangles");
+#ifndef NR_BIN_PREFETCH
+#define NR_BIN_PREFETCH 0   // 1: the positions are loaded before the cluster test (one latency round less, all bytes)
+#endif
+    f64 pxy[TPT][6];
+    if (NR_BIN_PREFETCH) {
+#pragma unroll
+        for (int k = 0; k < TPT; ++k) {
+            const i64 t = base + k * 256 + tid;
+            if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
+        }
+    }
     bool cl[TPT];
+    bool anyc = false;
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 c = (base + k * 256) / NR_CLUSTER + __builtin_amdgcn_readfirstlane(tid >> 6);
         cl[k] = !cbox || c * NR_CLUSTER >= bp.src.n || cluster_may_touch(bp, cbox + c * 4);
+        anyc = anyc || cl[k];
     }
-    f64 pxy[TPT][6];
+    // a workgroup none of whose clusters reaches an owned tile has nothing to do
+    // (most of them on a sharded frame's rank)
+    if (cbox && !__syncthreads_or(anyc ? 1 : 0)) return;
+    if (!NR_BIN_PREFETCH) {
 #pragma unroll
-    for (int k = 0; k < TPT; ++k) {
-        const i64 t = base + k * 256 + tid;
-        if (cl[k] && t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
+        for (int k = 0; k < TPT; ++k) {
+            const i64 t = base + k * 256 + tid;
+            if (cl[k] && t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
+        }
     }
     if (LDSH) {
         for (int b = tid; b < hbins; b += 256) hist[b] = 0;
