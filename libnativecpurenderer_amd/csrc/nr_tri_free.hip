@@ -757,6 +757,10 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     // a workgroup none of whose clusters reaches an owned tile has nothing to do
     // (most of them on a sharded frame's rank)
     if (cbox && !__syncthreads_or(anyc ? 1 : 0)) return;
+#ifndef NR_BIN_STOP
+#define NR_BIN_STOP 0   // timing probe builds only: 1/2/3 stop after the cluster test / the histogram / the reservation
+#endif
+    if (NR_BIN_STOP == 1) return;
     if (!NR_BIN_PREFETCH) {
 #pragma unroll
         for (int k = 0; k < TPT; ++k) {
@@ -787,6 +791,7 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
             for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[hrow + tx], 1u);
         }
     }
+    if (NR_BIN_STOP == 2) return;
     if (LDSH) {
         __syncthreads();
         for (int b = tid; b < hbins; b += 256) {   // reserve each touched tile's range once
@@ -804,6 +809,7 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
         }
         __syncthreads();
     }
+    if (NR_BIN_STOP == 3) return;
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
