@@ -1191,7 +1191,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __shared__ int sLast;
     __shared__ unsigned long long sFrag;
     if (!plan[3]) return;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // (uniform: the chunk loop is a scalar loop)
     const u32 nitems = plan[1];
     unsigned long long myFrags = 0;
     if (COUNT && tid == 0) sFrag = 0;
@@ -1277,8 +1278,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         // conditional load, or a use right after it, makes the compiler wait
         // for the loads in flight on the spot.
         auto list_at = [&](u32 c) -> u32 {
-            const u32 b = ls + c * cs + lane;
-            return list[c < nch && (u32)lane < cs && b < le ? b : ls];
+            const int ln = opaque_tid() & 63;   // (formed here: the lane index is not kept live across the item)
+            const u32 b = ls + c * cs + ln;
+            return list[c < nch && (u32)ln < cs && b < le ? b : ls];
         };
         // chunk c + NWV's triangle (loaded) and chunk c + 2 NWV's (in flight)
         u32 pt = list_at(wave), ptn = list_at(wave + NWV);
