@@ -110,6 +110,11 @@ struct TriScratch {
         hipEvent_t ready = nullptr;                      // the copies above are done (main stream)
         bool waitReady = false;                          // the next warm binning on the binning stream waits for it
         u32* herr = nullptr; u32* derr = nullptr;        // host-mapped: a warm binning found a tile over its range
+        // the binning blocks (1024 triangles) with a cluster that may reach an
+        // owned tile under this key: the warm binning launches only those
+        u32* blocks = nullptr; size_t blocks_cap = 0;
+        u32 nblocks = 0;
+        u64 blocksGen = 0;                               // gen the list was built for (0: none)
     } sched;
     int warmMode = 0;                       // 0 automatic (NR_WARM), 1 on, 2 off (SetWarmBinning)
     u64 warmBatches = 0;                    // batches binned warm (GetWarmBatchCount)
@@ -215,6 +220,7 @@ struct TriangleBuffer {
     // binning of a sharded frame skips the clusters that lie outside the
     // rank's tile rows without loading their triangles
     f64* cbox = nullptr;
+    std::vector<f64> hcbox;   // (host copy: the warm schedule's active binning blocks are found on the host)
 };
 constexpr int NR_CLUSTER = 64;
 

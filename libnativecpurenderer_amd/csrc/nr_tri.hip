@@ -275,6 +275,7 @@ TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f
         NR_CHECK(hipMalloc(&tb->cbox, cb.size() * sizeof(f64)));
         NR_CHECK(hipMemcpyAsync(tb->cbox, cb.data(), cb.size() * sizeof(f64), hipMemcpyHostToDevice, s));
         NR_CHECK(hipStreamSynchronize(s));
+        tb->hcbox = std::move(cb);
     }
     return tb;
 }

@@ -726,10 +726,13 @@ __device__ __forceinline__ bool cluster_may_touch(const BinParams& bp, const f64
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32* __restrict__ off,
                                                   u32* __restrict__ cur, u32* __restrict__ list,
-                                                  u32* __restrict__ err, u32 epoch, const f64* __restrict__ cbox) {
+                                                  u32* __restrict__ err, u32 epoch, const f64* __restrict__ cbox,
+                                                  const u32* __restrict__ blocks) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
-    const i64 base = (i64)blockIdx.x * 256 * TPT;
+    // (blocks: the schedule's active blocks, warm_blocks; the others hold no
+    // cluster that reaches an owned tile)
+    const i64 base = (i64)(blocks ? blocks[blockIdx.x] : blockIdx.x) * 256 * TPT;
     const int hbins = bp.hrows * bp.tiles_x;
     u32* hlim = hist + hbins;
     // this wave's cluster of each of its TPT triangle groups (NR_CLUSTER == 64:
@@ -1962,12 +1965,22 @@ static bool warm_on(const TriScratch& sc) {
     }();
     return sc.warmMode ? sc.warmMode == 1 : v != 0;
 }
-static bool warm_inline(i64 n) {
+// Warm binning inline (main stream, right before the raster) or beside the
+// previous raster (binning stream).  Inline when the rank's owned share of
+// the batch is large: 1M triangles unsharded 0.154 -> 0.140 ms per frame,
+// neutral at 2 shards; beside the raster for small batches (C2 0.065 ->
+// 0.058 ms) and for the smaller shares, whose active binning blocks fit
+// beside the raster (8-way 0.0505 -> 0.046-0.048 ms, 4-way -1 %;
+// profiles/r04/ab_warm_blocks.txt).
+static bool warm_inline(i64 n, int period, u64 mask) {
     static const int v = [] {
         const char* e = getenv("NR_WARM_INLINE");
         return e ? atoi(e) : 2;
     }();
-    return v == 2 ? n >= 65536 : v != 0;
+    if (v != 2) return v != 0;
+    const u64 m = period >= 64 ? mask : (mask & ((1ull << period) - 1ull));
+    const f64 share = period == 1 ? 1.0 : (f64)__builtin_popcountll(m) / (f64)period;
+    return n >= 65536 && (f64)n * share >= 300000.0;
 }
 
 // Keeps the tile offsets, work items and plan totals of a validated binning
@@ -2020,11 +2033,66 @@ static bool sched_matches(const TriScratch& sc, const TriangleBuffer* tb, const 
 
 // A warm batch: one binning kernel into the schedule's ranges (binning set
 // `si`: cursors and pair list), then k_vis over the schedule's items.
-static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinParams& bp, const f64* tbCbox) {
+// The binning blocks (256 * TPT triangles) of a schedule with a cluster that
+// may reach an owned tile: cluster_may_touch on the host over the buffer's
+// cluster boxes, widened by two rows and eight columns each side (a superset
+// of the device test, which still runs per wave).  Built once per schedule:
+// the warm binning of a rank then launches only these workgroups (an 8-way
+// share: about 1 in 7).
+static bool host_cluster_may_touch(const BinParams& bp, const f64* box) {
+    f64 y0 = INFINITY, y1 = -INFINITY, x0 = INFINITY, x1 = -INFINITY;
+    for (int c = 0; c < 4; ++c) {
+        f64 sx, sy;
+        nr_xform(bp.m, box[(c & 1) ? 2 : 0], box[(c & 2) ? 3 : 1], sx, sy);
+        if (!std::isfinite(sx) || !std::isfinite(sy)) return true;
+        y0 = std::min(y0, sy); y1 = std::max(y1, sy); x0 = std::min(x0, sx); x1 = std::max(x1, sx);
+    }
+    if (x1 < -12.0 || x0 > (f64)bp.W + 12.0) return false;
+    const f64 r0 = std::max(std::ceil(y0) - 3.0, 0.0), r1 = std::min(std::ceil(y1) + 3.0, (f64)bp.H);
+    if (!(r0 < r1)) return false;
+    if (bp.period == 1) return true;
+    const int ty0 = (int)r0 / TH, ty1 = ((int)r1 - 1) / TH;
+    if (ty1 >= ty0 + 64) return true;
+    for (int ty = ty0; ty <= ty1; ++ty)
+        if ((bp.mask >> (ty % bp.period)) & 1ull) return true;
+    return false;
+}
+static void warm_blocks(RenderContext* ctx, const BinParams& bp, const TriangleBuffer* tb) {
+    auto& S = ctx->tri.sched;
+    if (S.blocksGen == S.gen) return;
+    const i64 n = bp.src.n, per = 256 * TPT, nb = (n + per - 1) / per;
+    const i64 nc = (i64)tb->hcbox.size() / 4;
+    std::vector<u32> act;
+    act.reserve((size_t)nb);
+    for (i64 b = 0; b < nb; ++b) {
+        bool any = false;
+        for (i64 c = b * (per / NR_CLUSTER); c < std::min<i64>((b + 1) * (per / NR_CLUSTER), nc) && !any; ++c)
+            any = host_cluster_may_touch(bp, tb->hcbox.data() + c * 4);
+        if (any || nc == 0) act.push_back((u32)b);
+    }
+    if (S.blocks_cap < std::max<size_t>(act.size(), 1)) {
+        NR_CHECK(hipStreamSynchronize(ctx->stream));
+        NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
+        if (S.blocks) NR_CHECK(hipFree(S.blocks));
+        S.blocks_cap = std::max<size_t>((size_t)nb, 1);
+        NR_CHECK(hipMalloc(&S.blocks, S.blocks_cap * sizeof(u32)));
+    }
+    // (pageable source: the copy is staged before the call returns; ordered
+    // on the main stream before any warm binning of this schedule, S.ready)
+    if (!act.empty())
+        NR_CHECK(hipMemcpyAsync(S.blocks, act.data(), act.size() * sizeof(u32), hipMemcpyHostToDevice, ctx->stream));
+    NR_CHECK(hipEventRecord(S.ready, ctx->stream));
+    S.waitReady = true;
+    S.nblocks = (u32)act.size();
+    S.blocksGen = S.gen;
+}
+
+static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinParams& bp, const TriangleBuffer* tb) {
+    const f64* tbCbox = tb->cbox;
     TriScratch& sc = ctx->tri;
     auto& S = sc.sched;
     hipStream_t sa = ctx->stream;
-    hipStream_t sb = warm_inline(bp.src.n) ? sa : nr_bin_stream_for(ctx->device);
+    hipStream_t sb = warm_inline(bp.src.n, fp.period, fp.mask) ? sa : nr_bin_stream_for(ctx->device);
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % bin_sets();
@@ -2056,6 +2124,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         sc.fdone = db[0];
         if (sc.fdone_cap != olddone) NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.fdone_cap * sizeof(u32), sa));
     }
+    if (tbCbox) warm_blocks(ctx, bp, tb);
     if (F.visRecorded && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, F.evVis, 0));
     if (S.waitReady && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, S.ready, 0));
     S.waitReady = false;
@@ -2080,10 +2149,23 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         return e ? atoi(e) != 0 : true;
     }();
     const f64* cbox = cullOn ? tbCbox : nullptr;
-    if (ldsh) hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(gb), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
-                                    binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr, epoch, cbox);
-    else hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(gb), dim3(256), 0, sb, nullptr, binStop, 0, bp, (const u32*)S.off,
-                               F.fcur, F.flist, S.derr, epoch, cbox);
+    static const bool blocksOn = [] {   // NR_WARM_BLOCKS=0: launch every block (A/B)
+        const char* e = getenv("NR_WARM_BLOCKS");
+        return e ? atoi(e) != 0 : true;
+    }();
+    const bool useBlocks = blocksOn && cbox && S.blocksGen == S.gen;
+    const u32* blocks = useBlocks ? S.blocks : nullptr;
+    const int grid = useBlocks ? (int)S.nblocks : gb;
+    if (grid > 0) {
+        if (ldsh)
+            hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(grid), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
+                                  binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr, epoch, cbox, blocks);
+        else
+            hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(grid), dim3(256), 0, sb, nullptr, binStop, 0, bp,
+                                  (const u32*)S.off, F.fcur, F.flist, S.derr, epoch, cbox, blocks);
+    } else if (binStop) {
+        NR_CHECK(hipEventRecord(F.evBin, sb));
+    }
     NR_CHECK(hipGetLastError());
     nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
     if (sb != sa) {
@@ -2166,7 +2248,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     if (!ordered && !exact && sched_matches(sc, tb, key)) {
         if (sc.sched.herr && *(volatile u32*)sc.sched.herr)
             nr_set_error_msg("triangle batch: a warm binning found a tile over its kept range");
-        if (warm_enqueue(ctx, fp, bp, tb->cbox)) {
+        if (warm_enqueue(ctx, fp, bp, tb)) {
             ctx->lastPath = 1;
             ++sc.warmBatches;
             finish_batch(ctx, fp);
