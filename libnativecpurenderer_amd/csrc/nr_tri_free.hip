@@ -87,7 +87,7 @@ constexpr u32 SLICE = NR_SLICE;   // longest work item (triangles)
 #endif
 constexpr u32 SLICE_MIN = NR_SLICE_MIN;   // shortest slice of a split tile
 #ifndef NR_SLICE_TARGET
-#define NR_SLICE_TARGET 512
+#define NR_SLICE_TARGET 256   // round 4: 512 -> 256 (an 8-way share's slices 512 -> 1024: 0.046 -> 0.041 ms per frame)
 #endif
 constexpr int TPT = 4;       // triangles per thread in the binning kernels
 constexpr int LDS_HIST_MAX = 16384;
@@ -1644,6 +1644,11 @@ static void record_known(TriangleBuffer* tb, const BinKey& key, u32 pairs, u32 h
 
 // Items the plan kernel aims for when it picks the slice length
 // (NR_SLICE_TARGET; the environment variable of the same name overrides it).
+// Round 4 (warm binning, spill-free k_vis): 256, i.e. slices of 1024 for every
+// batch of >= 2^17 owned pairs.  An 8-way C3 share (~150k pairs) used to get
+// slices of 512: its split tiles' slot merges cost more than the longer
+// slices (0.046 -> 0.041 ms per frame, C2 -1 %, C3 unchanged;
+// profiles/r04/ab_slice_target.txt).
 static u32 slice_target() {
     static const u32 v = [] {
         const char* e = getenv("NR_SLICE_TARGET");
