@@ -6,6 +6,7 @@
 #   smoke           __graft_entry__.smoke()
 #   bench[:ARGS]    python bench.py ARGS  (ARGS: comma-separated, e.g. bench:--config,c2,--steps,20)
 #   trace[:ARGS]    rocprofv3 --kernel-trace --hip-runtime-trace of bench.py ARGS (+ timeline.py)
+#   ktrace[:ARGS]   rocprofv3 --kernel-trace of bench.py ARGS (+ timeline.py), no runtime trace
 #   stats[:ARGS]    rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   ab:ENV1%ENV2%.. bench lines under each environment (ENVk = A=1+B=2), twice, interleaved; BENCH_ARGS env for the bench flags
 #   py:SCRIPT,ARGS  python SCRIPT ARGS
@@ -39,6 +40,10 @@ for step in "$@"; do
     bench) run bench 600 python bench.py "${A[@]}" ;;
     trace) d="$OUT/trace$i"
            run trace 600 rocprofv3 --kernel-trace --hip-runtime-trace -d "$d" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra "${A[@]}"
+           kt=$(find "$d" -name '*kernel_trace.csv' | head -1)
+           [ -n "$kt" ] && python3 tools/timeline.py "$kt" 4 > "$OUT/$(printf %02d $i)_timeline.txt" 2>&1 ;;
+    ktrace) d="$OUT/ktrace$i"   # kernel trace only (no runtime trace: the host runs at full speed)
+           run ktrace 600 rocprofv3 --kernel-trace -d "$d" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra "${A[@]}"
            kt=$(find "$d" -name '*kernel_trace.csv' | head -1)
            [ -n "$kt" ] && python3 tools/timeline.py "$kt" 4 > "$OUT/$(printf %02d $i)_timeline.txt" 2>&1 ;;
     stats) d="$OUT/stats$i"
