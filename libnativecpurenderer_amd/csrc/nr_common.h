@@ -71,6 +71,10 @@ struct TriScratch {
         bool visRecorded = false;
         u64 curGen = 0;                     // fcur = curEpoch x the counts of schedule curGen (0: unknown)
         u32 curEpoch = 0;
+        // warm binning beside the raster: same-queue hand-off (k_gate_signal / k_gate_wait)
+        u32* gate = nullptr;                // [0] token of the set's last finished binning
+        u32* gplan = nullptr;               // the raster's plan words (k_gate_wait copies the schedule's)
+        u32 gateTok = 0;
     } fset[3];
     int fnext = 0;                          // set of the next batch
     u32* fdone = nullptr; size_t fdone_cap = 0;   // split-tile slice counters (k_vis only)

@@ -358,22 +358,33 @@ struct FrameParams {
 // clear): the u8 image (cpp:52-57) or, with fp.frameYUV, its YUV420P planes --
 // Y of every pixel, U and V from the even pixel of each 2x2 block (tiles have
 // even sizes and origins, so a block never straddles two).
+// Output stores of the rasters' shading passes (framebuffer, depth, frame
+// output): written once per frame and not read again by the kernel.
+// NR_NT_STORE=1: non-temporal (streaming) stores (A/B).
+#ifndef NR_NT_STORE
+#define NR_NT_STORE 0
+#endif
+template <class T>
+__device__ __forceinline__ void out_store(T* p, T v) {
+    if (NR_NT_STORE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 __device__ __forceinline__ void store_frame_out(const FrameParams& fp, i64 p, i64 px, i64 py, f64 cr, f64 cg, f64 cb,
                                                 f64 ca) {
     if (!fp.frameU8) return;
     const int r8 = nr_to_u8(cr), g8 = nr_to_u8(cg), b8 = nr_to_u8(cb);
     if (fp.frameYUV) {
-        fp.frameU8[p] = nr_y_of(r8, g8, b8);
+        out_store<iu8>(fp.frameU8 + p, (iu8)nr_y_of(r8, g8, b8));
         if (!((px | py) & 1)) {
             const i64 cw = fp.W >> 1;
             iu8* up = fp.frameU8 + fp.W * fp.H + (py >> 1) * cw + (px >> 1);
-            up[0] = nr_u_of(r8, g8, b8);
-            up[cw * (fp.H >> 1)] = nr_v_of(r8, g8, b8);
+            out_store<iu8>(up, (iu8)nr_u_of(r8, g8, b8));
+            out_store<iu8>(up + cw * (fp.H >> 1), (iu8)nr_v_of(r8, g8, b8));
         }
     } else {
         iu8* d8 = fp.frameU8 + p * fp.ipp;
-        d8[0] = (iu8)r8; d8[1] = (iu8)g8; d8[2] = (iu8)b8;
-        if (fp.ipp == 4) d8[3] = nr_to_u8(ca);
+        out_store<iu8>(d8, (iu8)r8); out_store<iu8>(d8 + 1, (iu8)g8); out_store<iu8>(d8 + 2, (iu8)b8);
+        if (fp.ipp == 4) out_store<iu8>(d8 + 3, (iu8)nr_to_u8(ca));
     }
 }
 

@@ -2038,6 +2038,46 @@ static bool sched_matches(const TriScratch& sc, const TriangleBuffer* tb, const 
 
 // A warm batch: one binning kernel into the schedule's ranges (binning set
 // `si`: cursors and pair list), then k_vis over the schedule's items.
+// Same-queue hand-off from a warm binning beside the raster to the raster
+// (NR_GATE, default on): the binning stream ends the batch's binning with
+// k_gate_signal storing the set's next token, and the main stream runs
+// k_gate_wait -- one thread polling the token -- right before the raster, in
+// place of a cross-queue event wait, whose wake-up cost ~10 us per frame
+// after a binning that had long finished (8-way share kernel trace,
+// profiles/r04/ab_any_order.txt).  The binning kernel's completion (kernel
+// boundary on the binning stream) makes its pairs visible before the token is
+// stored.  k_gate_wait also hands the raster its plan words (a copy of the
+// schedule's); should the token not arrive within a second, the copy says
+// "did not fit" (the raster does nothing) and the host latches an error --
+// no wave polls forever, no raster reads a half-written list.  The binning is
+// enqueued before the wait on the host, so even two streams sharing one
+// hardware queue cannot deadlock.
+__global__ void k_gate_signal(u32* __restrict__ gate, u32 tok) {
+    if (threadIdx.x == 0) __hip_atomic_store(gate, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_gate_wait(const u32* __restrict__ gate, u32 tok, const u32* __restrict__ splan,
+                            u32* __restrict__ gplan, u32* __restrict__ err) {
+    if (threadIdx.x != 0) return;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    bool ok = true;
+    while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+            ok = false;
+            break;
+        }
+    }
+    for (int k = 0; k < 4; ++k) gplan[k] = (k == 3 && !ok) ? 0u : splan[k];   // {pairs, items, slices, fits}
+    if (!ok) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+static bool gate_on() {   // NR_GATE=0: the cross-queue event wait (A/B)
+    static const bool v = [] {
+        const char* e = getenv("NR_GATE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // The binning blocks (256 * TPT triangles) of a schedule with a cluster that
 // may reach an owned tile: cluster_may_touch on the host over the buffer's
 // cluster boxes, widened by two rows and eight columns each side (a superset
@@ -2145,7 +2185,14 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const int gb = (int)((bp.src.n + 256 * TPT - 1) / (256 * TPT));
     hipEvent_t e0, e1;
     nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
-    const bool xs = ext_stop() && sb != sa && !e1;
+    const bool gated = sb != sa && gate_on() && !e1;   // same-queue hand-off (k_gate_wait) instead of an event wait
+    if (gated && !F.gate) {
+        NR_CHECK(hipMalloc(&F.gate, 4 * sizeof(u32)));
+        NR_CHECK(hipMalloc(&F.gplan, 4 * sizeof(u32)));
+        NR_CHECK(hipMemset(F.gate, 0, 4 * sizeof(u32)));
+        F.gateTok = 0;
+    }
+    const bool xs = ext_stop() && sb != sa && !e1 && !gated;
     hipEvent_t binStop = xs ? F.evBin : nullptr;
     const u32 epoch = F.curEpoch++;
     // cluster culling of the rank's tile rows (NR_CLUSTER_CULL=0: off, A/B)
@@ -2173,7 +2220,15 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     }
     NR_CHECK(hipGetLastError());
     nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
-    if (sb != sa) {
+    const u32* visPlan = S.dplan;
+    if (gated) {
+        if (++F.gateTok == 0) F.gateTok = 1;   // (the word starts at 0)
+        hipLaunchKernelGGL(k_gate_signal, dim3(1), dim3(64), 0, sb, F.gate, F.gateTok);
+        hipLaunchKernelGGL(k_gate_wait, dim3(1), dim3(64), 0, sa, (const u32*)F.gate, F.gateTok, (const u32*)S.dplan,
+                           F.gplan, S.derr);
+        NR_CHECK(hipGetLastError());
+        visPlan = F.gplan;
+    } else if (sb != sa) {
         if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
         NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
     }
@@ -2184,7 +2239,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (S.nitems > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = ext_stop() && !e1;
-        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, S.dplan}, std::min<u32>(S.nitems, 8192), sa,
+        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan}, std::min<u32>(S.nitems, 8192), sa,
                        vs ? F.evVis : nullptr, owned_share_large(fp.period, fp.mask, bp.src.n), zmode,
                        fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
@@ -2252,7 +2307,9 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     // warm: the schedule kept from this buffer's last validated binning under this key
     if (!ordered && !exact && sched_matches(sc, tb, key)) {
         if (sc.sched.herr && *(volatile u32*)sc.sched.herr)
-            nr_set_error_msg("triangle batch: a warm binning found a tile over its kept range");
+            nr_set_error_msg(*(volatile u32*)sc.sched.herr == 2
+                                 ? "triangle batch: a raster's wait for its warm binning timed out (NR_GATE)"
+                                 : "triangle batch: a warm binning found a tile over its kept range");
         if (warm_enqueue(ctx, fp, bp, tb)) {
             ctx->lastPath = 1;
             ++sc.warmBatches;

@@ -39,8 +39,8 @@ struct RecLen {
 // the winner's depth, or a pending depth clear.
 template <int ZMODE>
 __device__ __forceinline__ void store_depth(const FrameParams& fp, i64 p, u64 kv) {
-    if (ZMODE == 1 && (u32)kv) fp.depth[p] = (u32)(kv >> 32);
-    else if (ZMODE != 0 && fp.pendDepth) fp.depth[p] = fp.pendDepthValue;
+    if (ZMODE == 1 && (u32)kv) out_store<u32>(fp.depth + p, (u32)(kv >> 32));
+    else if (ZMODE != 0 && fp.pendDepth) out_store<u32>(fp.depth + p, fp.pendDepthValue);
 }
 
 // Framebuffer (+ frame output, nr_tri.h store_frame_out) value of pixel p =
@@ -49,8 +49,8 @@ __device__ __forceinline__ void store_colour(const FrameParams& fp, i64 p, i64 p
                                              f64 ca) {
     const int ipp = fp.ipp;
     f64* dst = fp.fb + p * ipp;
-    dst[0] = cr; dst[1] = cg; dst[2] = cb;
-    if (ipp == 4) dst[3] = ca;
+    out_store<f64>(dst, cr); out_store<f64>(dst + 1, cg); out_store<f64>(dst + 2, cb);
+    if (ipp == 4) out_store<f64>(dst + 3, ca);
     store_frame_out(fp, p, px, py, cr, cg, cb, ca);
 }
 
