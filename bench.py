@@ -396,7 +396,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=200,
+                    help="untimed frames first: the GPU needs ~30 ms of load to reach its steady clocks "
+                         "(10 frames left a 20-step C3 timed region ~3 %% slow, profiles/r04/warmup_steps20.txt)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", dest="extra", action="store_true", default=None,
