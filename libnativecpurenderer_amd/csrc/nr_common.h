@@ -119,6 +119,7 @@ struct TriScratch {
         u32* blocks = nullptr; size_t blocks_cap = 0;
         u32 nblocks = 0;
         u64 blocksGen = 0;                               // gen the list was built for (0: none)
+        bool anyCull = true;                             // some cluster may lie off the owned tiles (else no device test)
     } sched;
     int warmMode = 0;                       // 0 automatic (NR_WARM), 1 on, 2 off (SetWarmBinning)
     u64 warmBatches = 0;                    // batches binned warm (GetWarmBatchCount)

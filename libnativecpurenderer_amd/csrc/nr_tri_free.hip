@@ -2109,12 +2109,19 @@ static void warm_blocks(RenderContext* ctx, const BinParams& bp, const TriangleB
     const i64 nc = (i64)tb->hcbox.size() / 4;
     std::vector<u32> act;
     act.reserve((size_t)nb);
+    bool anyCull = false;
     for (i64 b = 0; b < nb; ++b) {
         bool any = false;
-        for (i64 c = b * (per / NR_CLUSTER); c < std::min<i64>((b + 1) * (per / NR_CLUSTER), nc) && !any; ++c)
-            any = host_cluster_may_touch(bp, tb->hcbox.data() + c * 4);
+        for (i64 c = b * (per / NR_CLUSTER); c < std::min<i64>((b + 1) * (per / NR_CLUSTER), nc); ++c) {
+            const bool t = host_cluster_may_touch(bp, tb->hcbox.data() + c * 4);
+            any = any || t;
+            anyCull = anyCull || !t;
+        }
         if (any || nc == 0) act.push_back((u32)b);
     }
+    // every cluster may reach an owned tile (an unsharded frame with the mesh
+    // on screen): the device's cluster tests could cull nothing worth a test
+    S.anyCull = anyCull;
     if (S.blocks_cap < std::max<size_t>(act.size(), 1)) {
         NR_CHECK(hipStreamSynchronize(ctx->stream));
         NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
@@ -2200,7 +2207,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         const char* e = getenv("NR_CLUSTER_CULL");
         return e ? atoi(e) != 0 : true;
     }();
-    const f64* cbox = cullOn ? tbCbox : nullptr;
+    const f64* cbox = cullOn && S.anyCull ? tbCbox : nullptr;
     static const bool blocksOn = [] {   // NR_WARM_BLOCKS=0: launch every block (A/B)
         const char* e = getenv("NR_WARM_BLOCKS");
         return e ? atoi(e) != 0 : true;
