@@ -89,7 +89,10 @@ constexpr u32 SLICE_MIN = NR_SLICE_MIN;   // shortest slice of a split tile
 #ifndef NR_SLICE_TARGET
 #define NR_SLICE_TARGET 256   // round 4: 512 -> 256 (an 8-way share's slices 512 -> 1024: 0.046 -> 0.041 ms per frame)
 #endif
-constexpr int TPT = 4;       // triangles per thread in the binning kernels
+#ifndef NR_TPT
+#define NR_TPT 4
+#endif
+constexpr int TPT = NR_TPT;   // triangles per thread in the binning kernels
 constexpr int LDS_HIST_MAX = 16384;
 
 // Tile rectangle of a triangle, packed for the emit pass (16 bits per bound;
