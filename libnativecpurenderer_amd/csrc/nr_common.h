@@ -117,6 +117,7 @@ struct TriScratch {
         // the binning blocks (1024 triangles) with a cluster that may reach an
         // owned tile under this key: the warm binning launches only those
         u32* blocks = nullptr; size_t blocks_cap = 0;
+        std::vector<u32> hblocks;                        // (host source of the last upload, kept alive)
         u32 nblocks = 0;
         u64 blocksGen = 0;                               // gen the list was built for (0: none)
         bool anyCull = true;                             // some cluster may lie off the owned tiles (else no device test)

@@ -2110,7 +2110,12 @@ static void warm_blocks(RenderContext* ctx, const BinParams& bp, const TriangleB
     if (S.blocksGen == S.gen) return;
     const i64 n = bp.src.n, per = 256 * TPT, nb = (n + per - 1) / per;
     const i64 nc = (i64)tb->hcbox.size() / 4;
-    std::vector<u32> act;
+    // (the previous upload from this vector was ordered before any warm
+    // binning of the previous schedule, all of which the sync below or the
+    // stream order has passed)
+    NR_CHECK(hipStreamSynchronize(ctx->stream));
+    std::vector<u32>& act = S.hblocks;
+    act.clear();
     act.reserve((size_t)nb);
     bool anyCull = false;
     for (i64 b = 0; b < nb; ++b) {
@@ -2126,14 +2131,12 @@ static void warm_blocks(RenderContext* ctx, const BinParams& bp, const TriangleB
     // on screen): the device's cluster tests could cull nothing worth a test
     S.anyCull = anyCull;
     if (S.blocks_cap < std::max<size_t>(act.size(), 1)) {
-        NR_CHECK(hipStreamSynchronize(ctx->stream));
         NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
         if (S.blocks) NR_CHECK(hipFree(S.blocks));
         S.blocks_cap = std::max<size_t>((size_t)nb, 1);
         NR_CHECK(hipMalloc(&S.blocks, S.blocks_cap * sizeof(u32)));
     }
-    // (pageable source: the copy is staged before the call returns; ordered
-    // on the main stream before any warm binning of this schedule, S.ready)
+    // (ordered on the main stream before any warm binning of this schedule, S.ready)
     if (!act.empty())
         NR_CHECK(hipMemcpyAsync(S.blocks, act.data(), act.size() * sizeof(u32), hipMemcpyHostToDevice, ctx->stream));
     NR_CHECK(hipEventRecord(S.ready, ctx->stream));
