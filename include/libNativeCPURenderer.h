@@ -153,6 +153,9 @@ void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW:
 void SetFrameVisRaster(RenderContext* ctx, i64 mode);                    /* NEW: frame visibility buffer 0 auto, 1 on, 2 off */
 void SetWarmBinning(RenderContext* ctx, i64 mode);                       /* NEW: one-pass binning of a repeat draw 0 auto, 1 on, 2 off */
 i64 GetWarmBatchCount(RenderContext* ctx);                               /* NEW (testing): batches binned warm */
+void SetWarmFaultInjection(RenderContext* ctx, i64 mode);                /* NEW (testing): fault in the next warm batch
+                                 1 range overflow, 2 withheld token, 3 dropped pairs (the frame must stay exact) */
+i64 GetWarmFailureCount(RenderContext* ctx);                             /* NEW (testing): warm batches that failed a check */
 void SetSplitLimits(RenderContext* ctx, i64 splitAt, i64 dslice);       /* NEW: dense-tile split limits (0: defaults) */
 
 /* ---- NEW: multi-GPU frames (tile-row sharding + RCCL assembly) */

@@ -85,6 +85,8 @@ DEVICE_ABI = {
     "SetFrameVisRaster": (None, (P, L)),
     "SetWarmBinning": (None, (P, L)),
     "GetWarmBatchCount": (L, (P,)),
+    "SetWarmFaultInjection": (None, (P, L)),
+    "GetWarmFailureCount": (L, (P,)),
     "SetSplitLimits": (None, (P, L, L)),
     "GetLastErrorString": (ctypes.c_char_p, ()),
     "ClearLastError": (None, ()),

@@ -379,12 +379,12 @@ void DestroyRenderContext(RenderContext* ctx) {
         if (F.evVis) NR_CHECK(hipEventDestroy(F.evVis));
     }
     if (t.h_total) NR_CHECK(hipHostFree(t.h_total));
+    if (t.hfail) NR_CHECK(hipHostFree(t.hfail));
     {   // the warm-binning schedule
         auto& S = t.sched;
         void* sp[] = {S.off, S.items, S.dplan, S.blocks};
         for (void* p : sp)
             if (p) NR_CHECK(hipFree(p));
-        if (S.herr) NR_CHECK(hipHostFree(S.herr));
         if (S.ready) NR_CHECK(hipEventDestroy(S.ready));
     }
     for (auto& p : ctx->evPending) {

@@ -113,7 +113,6 @@ struct TriScratch {
         u64 gen = 0;                                     // process-unique generation of this schedule
         hipEvent_t ready = nullptr;                      // the copies above are done (main stream)
         bool waitReady = false;                          // the next warm binning on the binning stream waits for it
-        u32* herr = nullptr; u32* derr = nullptr;        // host-mapped: a warm binning found a tile over its range
         // the binning blocks (1024 triangles) with a cluster that may reach an
         // owned tile under this key: the warm binning launches only those
         u32* blocks = nullptr; size_t blocks_cap = 0;
@@ -124,6 +123,14 @@ struct TriScratch {
     } sched;
     int warmMode = 0;                       // 0 automatic (NR_WARM), 1 on, 2 off (SetWarmBinning)
     u64 warmBatches = 0;                    // batches binned warm (GetWarmBatchCount)
+    // warm-batch checks (k_vis WarmCheck): host-mapped word a raster sets when
+    // a warm batch failed them (1 binning check, 2 token timeout), read by
+    // nr_settle; the batch itself was rasterised from all its triangles
+    u32* hfail = nullptr; u32* dfail = nullptr;
+    u32 warmTag = 0;                        // tag of the last warm batch (k_bin_warm's error word)
+    u64 warmFailures = 0;                   // warm batches that failed their checks (GetWarmFailureCount)
+    std::vector<u64> warmBanned;            // buffers (uid) whose warm binning failed a check: binned cold
+    int warmInject = 0;                     // testing: fault injected into the next warm batch (SetWarmFaultInjection)
     f64 srcMeanArea = -1;                   // mean |signed area| of the batch being drawn, user space (-1: unknown)
 };
 

@@ -323,6 +323,18 @@ void SetFrameVisRaster(RenderContext* ctx, i64 mode) { ctx->tri.gvisMode = (int)
 void SetWarmBinning(RenderContext* ctx, i64 mode) { ctx->tri.warmMode = (int)(mode >= 0 && mode <= 2 ? mode : 0); }
 // New (testing): number of batches of this context binned warm so far.
 i64 GetWarmBatchCount(RenderContext* ctx) { return (i64)ctx->tri.warmBatches; }
+// New (testing): a fault in the next warm batch -- 1 its binning finds its
+// tiles over their ranges, 2 (a batch binned beside the raster) its token is
+// withheld (the raster's wait times out after 1 s), 3 it drops a workgroup's
+// pairs.  The raster must then run its fallback (k_vis WarmCheck): the frame
+// stays exact and the failure is latched (GetWarmFailureCount, the error).
+void SetWarmFaultInjection(RenderContext* ctx, i64 mode) { ctx->tri.warmInject = (int)(mode >= 0 && mode <= 3 ? mode : 0); }
+// New (testing): warm batches whose checks failed so far (read at API calls).
+i64 GetWarmFailureCount(RenderContext* ctx) {
+    NR_CHECK(hipSetDevice(ctx->device));
+    nrtri::settle(ctx);
+    return (i64)ctx->tri.warmFailures;
+}
 
 // New: which raster the last batch took (1 = order-free tiled, 2 = ordered, 3 = order-free frame buffer).
 i64 GetLastRasterPath(RenderContext* ctx) { return ctx->lastPath; }

@@ -32,6 +32,7 @@
 
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -696,27 +697,39 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 // k_free_emit) -- into the same [off[t], off[t + 1]) ranges: the count pass,
 // the plan and the host's validation of the cold path are not needed,
 // because the same buffer under the same key gives every tile exactly its
-// former count.  (A tile found over its range -- not possible -- sets *err and
-// its excess pairs are dropped.)  LDSH: hist (next slot) and hlim (range end)
-// per owned tile in LDS.
+// former count.  LDSH: hist (next slot) and hlim (range end) per owned tile in
+// LDS.
 // The set's pair cursors are not reset between warm batches: the epoch-th
 // warm batch of one schedule on this set finds cur[t] = epoch * count(t) and
 // takes slots from there (cursor - epoch * count, count = off[t + 1] - off[t]).
+// Checks (wstat, beside the cursors): a tile found over its range stores the
+// batch's tag in wstat[WS_TAG] (its excess pairs are dropped), and every
+// workgroup adds its pair total to wstat[WS_SUM] (zeroed with the cursors),
+// which after the e-th warm batch must equal
+// (e + 1) * the schedule's pairs -- so an undercount anywhere is seen too.
+// k_vis reads both before it trusts the lists (WarmCheck).  `inject` (tests
+// only, SetWarmFaultInjection): 1 shifts the epoch (every touched tile out of
+// its range), 3 drops workgroup 0's pairs (an undercount).
 // Can a cluster (user-space box {xmin, ymin, xmax, ymax}, TriangleBuffer::cbox)
 // put a pair into an owned tile?  Its corners' screen positions bound every
 // vertex's (the affine map's rounded products and sums are monotone in x and
 // y), so a triangle's rows [ceil(ymin), ceil(ymax)) lie in the corners' row
 // range (one row of margin each side); non-finite boxes are never culled.
+// Columns follow tri_tiles: a triangle with a screen coordinate beyond 1e7
+// is binned into every column of its rows, so a box with a corner beyond
+// 1e7 (which may hold such a vertex) is never culled by x.
 __device__ __forceinline__ bool cluster_may_touch(const BinParams& bp, const f64* box) {
     f64 y0 = INFINITY, y1 = -INFINITY, x0 = INFINITY, x1 = -INFINITY;
+    bool huge = false;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         f64 sx, sy;
         nr_xform(bp.m, box[(c & 1) ? 2 : 0], box[(c & 2) ? 3 : 1], sx, sy);
         if (!isfinite(sx) || !isfinite(sy)) return true;
+        huge = huge || fabs(sx) > 1e7 || fabs(sy) > 1e7;
         y0 = fmin(y0, sy); y1 = fmax(y1, sy); x0 = fmin(x0, sx); x1 = fmax(x1, sx);
     }
-    if (x1 < -4.0 || x0 > (f64)bp.W + 4.0) return false;
+    if (!huge && (x1 < -4.0 || x0 > (f64)bp.W + 4.0)) return false;
     const f64 r0 = fmax(ceil(y0) - 1.0, 0.0), r1 = fmin(ceil(y1) + 1.0, (f64)bp.H);
     if (!(r0 < r1)) return false;
     if (bp.period == 1) return true;
@@ -726,13 +739,18 @@ __device__ __forceinline__ bool cluster_may_touch(const BinParams& bp, const f64
     return ty1 >= ty0 + 64;
 }
 
+enum { WS_SUM = 0, WS_TAG = 1 };   // the warm checks' words, right after a set's ntiles cursors
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32* __restrict__ off,
                                                   u32* __restrict__ cur, u32* __restrict__ list,
-                                                  u32* __restrict__ err, u32 epoch, const f64* __restrict__ cbox,
-                                                  const u32* __restrict__ blocks) {
+                                                  u32* __restrict__ wstat, u32 tag, u32 epoch,
+                                                  const f64* __restrict__ cbox, const u32* __restrict__ blocks,
+                                                  u32 inject) {
     extern __shared__ u32 hist[];
+    __shared__ u32 wgPairs;
     const int tid = threadIdx.x;
+    if (inject == 1) epoch += 7;
+    if (inject == 3 && blockIdx.x == 0) return;
     // (blocks: the schedule's active blocks, warm_blocks; the others hold no
     // cluster that reaches an owned tile)
     const i64 base = (i64)(blocks ? blocks[blockIdx.x] : blockIdx.x) * 256 * TPT;
@@ -767,6 +785,7 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
 #define NR_BIN_STOP 0   // timing probe builds only: 1/2/3 stop after the cluster test / the histogram / the reservation
 #endif
     if (NR_BIN_STOP == 1) return;
+    if (tid == 0) wgPairs = 0;
     if (!NR_BIN_PREFETCH) {
 #pragma unroll
         for (int k = 0; k < TPT; ++k) {
@@ -774,11 +793,10 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
             if (cl[k] && t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
         }
     }
-    if (LDSH) {
-        for (int b = tid; b < hbins; b += 256) hist[b] = 0;
-        __syncthreads();
-    }
+    if (LDSH) for (int b = tid; b < hbins; b += 256) hist[b] = 0;
+    __syncthreads();   // (hist and wgPairs zeroed)
     u64 rk[TPT];
+    u32 myPairs = 0;
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
@@ -790,14 +808,21 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
         int tx0, tx1, ty0, ty1;
         if (!tri_tiles(sx, sy, bp.W, bp.H, tx0, tx1, ty0, ty1)) continue;
         rk[k] = pack_rect(tx0, tx1, ty0, ty1);
-        if (!LDSH) continue;
         for (int ty = ty0; ty <= ty1; ++ty) {
             if (!owned_row(ty, bp.period, bp.mask)) continue;
+            myPairs += (u32)(tx1 - tx0 + 1);
+            if (!LDSH) continue;
             const int hrow = owned_ord(bp, ty) * bp.tiles_x;
             for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[hrow + tx], 1u);
         }
     }
     if (NR_BIN_STOP == 2) return;
+    {   // the workgroup's pair total (one global atomic)
+        u32 wp = myPairs;
+        wp += __shfl_xor(wp, 32); wp += __shfl_xor(wp, 16); wp += __shfl_xor(wp, 8);
+        wp += __shfl_xor(wp, 4); wp += __shfl_xor(wp, 2); wp += __shfl_xor(wp, 1);
+        if ((tid & 63) == 0 && wp) atomicAdd(&wgPairs, wp);
+    }
     if (LDSH) {
         __syncthreads();
         for (int b = tid; b < hbins; b += 256) {   // reserve each touched tile's range once
@@ -810,11 +835,12 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
                 const bool bad = start < beg || start + h > end;
                 hist[b] = bad ? end : start;   // (bad: every slot of this range fails slot < end)
                 hlim[b] = end;
-                if (bad) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (bad) __hip_atomic_store(&wstat[WS_TAG], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        __syncthreads();
     }
+    __syncthreads();   // (LDS ranges reserved; wgPairs complete)
+    if (tid == 0 && wgPairs) atomicAdd(&wstat[WS_SUM], wgPairs);
     if (NR_BIN_STOP == 3) return;
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
@@ -836,7 +862,7 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
                     end = off[hrow + tx + 1];
                     slot = beg + atomicAdd(&cur[hrow + tx], 1u) - epoch * (end - beg);
                     if (slot < beg || slot >= end) {
-                        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(&wstat[WS_TAG], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         slot = end;
                     }
                 }
@@ -1176,11 +1202,28 @@ constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 // items are latency-bound: more waves per item).
 // WPE: waves per SIMD the registers are allocated for (NR_VIS_WAVES_PER_EU, or 3 for large batches: see
 // launch_vis).
+// The checks of a warm batch (k_bin_warm): wstat = {pair sum of the set's
+// warm batches since its cursors were zeroed, tag of a batch that found a tile
+// over its range}; the lists are trusted when the sum == expect, the tag word
+// != this batch's tag and the plan says it fits (plan[3] == 0: the binning's token never
+// came, k_gate_wait).  Otherwise the raster runs its work items over EVERY
+// triangle of the batch instead of the tile lists -- slow, but the same frame
+// bit for bit (a triangle that misses a tile adds nothing to it) -- and
+// workgroup 0 reports the reason in host-mapped *hfail (1 binning check, 2
+// token timeout; nr_settle latches an error and drops the schedule).  wstat
+// null: a cold batch (plan[3] == 0 there: the batch does nothing, the host
+// re-runs it).
+struct WarmCheck {
+    const u32* wstat;
+    u32 tag, expect;
+    u32* hfail;
+};
+
 template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT, int WPE = NR_VIS_WAVES_PER_EU>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ kslot, u32* __restrict__ done,
-                                             const u32* __restrict__ plan) {
+                                             const u32* __restrict__ plan, const WarmCheck wc) {
     constexpr bool DEPTH = ZMODE != 0;
     constexpr int NWV = NT / 64;   // waves per workgroup
     // tile keys, rows padded to KS = 65 entries: lanes working on different
@@ -1196,7 +1239,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __shared__ u32 nU;
     __shared__ int sLast;
     __shared__ unsigned long long sFrag;
-    if (!plan[3]) return;
+    bool fb = false;   // fallback: every triangle of the batch against every tile (WarmCheck)
+    if (wc.wstat) {
+        const u32 wt = __hip_atomic_load(&wc.wstat[WS_TAG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u32 ws = __hip_atomic_load(&wc.wstat[WS_SUM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fb = !plan[3] || wt == wc.tag || ws != wc.expect;
+        if (fb && blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(wc.hfail, plan[3] ? 1u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (!plan[3]) {
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // (uniform: the chunk loop is a scalar loop)
     const u32 nitems = plan[1];
@@ -1223,9 +1275,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         __syncthreads();
         const int itid = opaque_tid();   // (this item's per-pixel addresses: formed here, not kept live)
         const int tile = (int)d.x;
-        const u32 ls = d.y, le = d.z;
+        u32 ls = d.y, le = d.z;
         const u32 nsl = d.w & 0xFFFFu;   // slices of the tile (d.w >> 16: this item's slice)
         const bool multi = nsl > 1;
+        if (fb) {   // this item's slice of all n triangles (never empty: a split tile has n >= its pairs > nsl)
+            const u64 n = (u64)fp.src.n, k = d.w >> 16;
+            ls = (u32)(k * n / nsl);
+            le = (u32)((k + 1) * n / nsl);
+        }
         constexpr int rlo = 0;
 #if NR_HEAVY_PRIO
         // the longest work items (dense tiles' slices) set the kernel's
@@ -1242,7 +1299,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
         const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
         const int rcap = hlim;   // rows [rlo, rcap) of the tile are rasterised here
-        if (ls == le) {   // no triangle: only the pending clears
+        if (ls == le && !multi) {   // no triangle: only the pending clears
             for (int p = itid; p < TH * TW; p += NT) {
                 const int lx = p & (TW - 1), ly = p / TW;
                 if (lx < wlim && ly < hlim)
@@ -1286,7 +1343,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         auto list_at = [&](u32 c) -> u32 {
             const int ln = opaque_tid() & 63;   // (formed here: the lane index is not kept live across the item)
             const u32 b = ls + c * cs + ln;
-            return list[c < nch && (u32)ln < cs && b < le ? b : ls];
+            const u32 i = c < nch && (u32)ln < cs && b < le ? b : ls;
+            return fb ? i : list[i];   // (fallback: the slice's triangle ids themselves)
         };
         // chunk c + NWV's triangle (loaded) and chunk c + 2 NWV's (in flight)
         u32 pt = list_at(wave), ptn = list_at(wave + NWV);
@@ -1560,11 +1618,13 @@ struct VisArgs {
     const uint4* items;
     const u32* list;
     const u32* plan;
+    WarmCheck wc;   // (a warm batch's checks; zero: a cold batch)
 };
 
 template <int Z, bool C, bool G>
 void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
                 hipEvent_t stop, bool big) {
+    const WarmCheck wc = va.wc;
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
     const bool coop = sc.coopMode ? sc.coopMode == 1
@@ -1574,7 +1634,7 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
     const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wide_heavy();
 #define NR_VIS(CO, NTT, ...)                                                                                       \
     hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, nullptr, stop, 0, fp, va.items,  \
-                          va.list, sc.kslot, sc.fdone, va.plan)
+                          va.list, sc.kslot, sc.fdone, va.plan, wc)
     if (wide) {
         if (coop) NR_VIS(1, 2 * VWG, false, G, true, 2 * VWG);
         else NR_VIS(0, 2 * VWG, false, G, false, 2 * VWG);
@@ -1948,7 +2008,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         const bool vs = ext_stop() && !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
         const bool largeShare = owned_share_large(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
-        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan}, grid, sa, st, largeShare, zmode, g);
+        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, 0u, 0u, nullptr}}, grid, sa, st, largeShare, zmode, g);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
@@ -2014,11 +2074,6 @@ static void sched_capture(RenderContext* ctx, TriScratch::FreeSet& F, const BinK
         if (!S.dplan) NR_CHECK(hipMalloc(&S.dplan, 4 * sizeof(u32)));
     }
     if (!S.ready) S.ready = sync_event();
-    if (!S.herr) {
-        NR_CHECK(hipHostMalloc((void**)&S.herr, sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
-        *S.herr = 0;
-        NR_CHECK(hipHostGetDevicePointer((void**)&S.derr, S.herr, 0));
-    }
     NR_CHECK(hipMemcpyAsync(S.off, F.foff, ((size_t)ntiles + 1) * sizeof(u32), hipMemcpyDeviceToDevice, sa));
     if (items) NR_CHECK(hipMemcpyAsync(S.items, F.fitems, (size_t)items * sizeof(uint4), hipMemcpyDeviceToDevice, sa));
     NR_CHECK(hipMemcpyAsync(S.dplan, F.dplan, 4 * sizeof(u32), hipMemcpyDeviceToDevice, sa));
@@ -2036,7 +2091,27 @@ static void sched_capture(RenderContext* ctx, TriScratch::FreeSet& F, const BinK
 
 static bool sched_matches(const TriScratch& sc, const TriangleBuffer* tb, const BinKey& key) {
     return warm_on(sc) && tb && sc.sched.valid && sc.sched.tbUid == tb->uid && !sc.capOverride &&
-           memcmp(&sc.sched.key, &key, sizeof key) == 0;
+           memcmp(&sc.sched.key, &key, sizeof key) == 0 &&
+           std::find(sc.warmBanned.begin(), sc.warmBanned.end(), tb->uid) == sc.warmBanned.end();
+}
+
+// A warm batch that failed its checks (k_vis WarmCheck: the raster then ran
+// over every triangle, so its frame is right) -- read at the next call into
+// the context: latch an error, drop the schedule (the next draw bins cold),
+// and after a binning-check failure bin that buffer cold from now on.
+static void warm_poll(RenderContext* ctx) {
+    TriScratch& sc = ctx->tri;
+    if (!sc.hfail) return;
+    const u32 f = __atomic_load_n(sc.hfail, __ATOMIC_ACQUIRE);
+    if (!f) return;
+    __atomic_store_n(sc.hfail, 0u, __ATOMIC_RELEASE);
+    ++sc.warmFailures;
+    if (f == 1 && sc.sched.valid) sc.warmBanned.push_back(sc.sched.tbUid);
+    sc.sched.valid = false;
+    nr_set_error_msg(f == 2 ? "triangle batch: a raster's wait for its warm binning timed out; "
+                              "the batch was rasterised from all its triangles"
+                            : "triangle batch: a warm binning failed its range / pair-count check; "
+                              "the batch was rasterised from all its triangles and the buffer bins cold from now on");
 }
 
 // A warm batch: one binning kernel into the schedule's ranges (binning set
@@ -2054,12 +2129,13 @@ static bool sched_matches(const TriScratch& sc, const TriangleBuffer* tb, const 
 // "did not fit" (the raster does nothing) and the host latches an error --
 // no wave polls forever, no raster reads a half-written list.  The binning is
 // enqueued before the wait on the host, so even two streams sharing one
-// hardware queue cannot deadlock.
+// hardware queue cannot deadlock.  (A timed-out raster runs its fallback and
+// reports, WarmCheck.)
 __global__ void k_gate_signal(u32* __restrict__ gate, u32 tok) {
     if (threadIdx.x == 0) __hip_atomic_store(gate, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void k_gate_wait(const u32* __restrict__ gate, u32 tok, const u32* __restrict__ splan,
-                            u32* __restrict__ gplan, u32* __restrict__ err) {
+                            u32* __restrict__ gplan) {
     if (threadIdx.x != 0) return;
     const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
     bool ok = true;
@@ -2071,7 +2147,6 @@ __global__ void k_gate_wait(const u32* __restrict__ gate, u32 tok, const u32* __
         }
     }
     for (int k = 0; k < 4; ++k) gplan[k] = (k == 3 && !ok) ? 0u : splan[k];   // {pairs, items, slices, fits}
-    if (!ok) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static bool gate_on() {   // NR_GATE=0: the cross-queue event wait (A/B)
     static const bool v = [] {
@@ -2089,13 +2164,15 @@ static bool gate_on() {   // NR_GATE=0: the cross-queue event wait (A/B)
 // share: about 1 in 7).
 static bool host_cluster_may_touch(const BinParams& bp, const f64* box) {
     f64 y0 = INFINITY, y1 = -INFINITY, x0 = INFINITY, x1 = -INFINITY;
+    bool huge = false;   // (tri_tiles' full-width rule, as the device test)
     for (int c = 0; c < 4; ++c) {
         f64 sx, sy;
         nr_xform(bp.m, box[(c & 1) ? 2 : 0], box[(c & 2) ? 3 : 1], sx, sy);
         if (!std::isfinite(sx) || !std::isfinite(sy)) return true;
+        huge = huge || std::fabs(sx) > 5e6 || std::fabs(sy) > 5e6;
         y0 = std::min(y0, sy); y1 = std::max(y1, sy); x0 = std::min(x0, sx); x1 = std::max(x1, sx);
     }
-    if (x1 < -12.0 || x0 > (f64)bp.W + 12.0) return false;
+    if (!huge && (x1 < -12.0 || x0 > (f64)bp.W + 12.0)) return false;
     const f64 r0 = std::max(std::ceil(y0) - 3.0, 0.0), r1 = std::min(std::ceil(y1) + 3.0, (f64)bp.H);
     if (!(r0 < r1)) return false;
     if (bp.period == 1) return true;
@@ -2156,7 +2233,13 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     sc.fnext = (sc.fnext + 1) % bin_sets();
     TriScratch::FreeSet& F = sc.fset[si];
     if (!F.evBin) { F.evBin = sync_event(); F.evVis = sync_event(); }
-    const size_t tneed = std::max<size_t>((size_t)ntiles + 1, TILE_ARR);
+    if (!sc.hfail) {
+        NR_CHECK(hipHostMalloc((void**)&sc.hfail, sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
+        *sc.hfail = 0;
+        NR_CHECK(hipHostGetDevicePointer((void**)&sc.dfail, sc.hfail, 0));
+    }
+    // cursors [0, ntiles), then the batch checks {error tag, pair sum} (WarmCheck)
+    const size_t tneed = std::max<size_t>((size_t)ntiles + 2, TILE_ARR);
     const bool grow = F.ftile_cap < tneed || !F.fcnt || F.flist_cap < std::max<size_t>(S.pairs, 1) ||
                       sc.kslot_cap < std::max<size_t>(S.split, 1) * (TH * TW) || sc.fdone_cap < (size_t)ntiles + 1;
     if (grow) {   // (first use of a set, or a larger schedule: rare)
@@ -2189,7 +2272,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     // cursors: epoch e of this schedule on this set (k_bin_warm); zeroed for a
     // new schedule, after a cold batch on the set, or before they could wrap
     if (F.curGen != S.gen || (u64)(F.curEpoch + 1) * std::max<u32>(S.pairs, 1) >= 0xF0000000ull) {
-        NR_CHECK(hipMemsetAsync(F.fcur, 0, (size_t)ntiles * sizeof(u32), sb));
+        NR_CHECK(hipMemsetAsync(F.fcur, 0, ((size_t)ntiles + 1) * sizeof(u32), sb));   // (and the pair sum)
         F.curGen = S.gen;
         F.curEpoch = 0;
     }
@@ -2208,6 +2291,11 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const bool xs = ext_stop() && sb != sa && !e1 && !gated;
     hipEvent_t binStop = xs ? F.evBin : nullptr;
     const u32 epoch = F.curEpoch++;
+    if (++sc.warmTag == 0) sc.warmTag = 1;
+    const u32 tag = sc.warmTag;
+    u32* const wstat = F.fcur + ntiles;   // {pair sum, error tag} (WS_SUM, WS_TAG)
+    const int inject = sc.warmInject;
+    sc.warmInject = 0;
     // cluster culling of the rank's tile rows (NR_CLUSTER_CULL=0: off, A/B)
     static const bool cullOn = [] {
         const char* e = getenv("NR_CLUSTER_CULL");
@@ -2224,10 +2312,11 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (grid > 0) {
         if (ldsh)
             hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(grid), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
-                                  binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, S.derr, epoch, cbox, blocks);
+                                  binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, wstat, tag, epoch, cbox, blocks,
+                                  (u32)inject);
         else
             hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(grid), dim3(256), 0, sb, nullptr, binStop, 0, bp,
-                                  (const u32*)S.off, F.fcur, F.flist, S.derr, epoch, cbox, blocks);
+                                  (const u32*)S.off, F.fcur, F.flist, wstat, tag, epoch, cbox, blocks, (u32)inject);
     } else if (binStop) {
         NR_CHECK(hipEventRecord(F.evBin, sb));
     }
@@ -2236,9 +2325,10 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const u32* visPlan = S.dplan;
     if (gated) {
         if (++F.gateTok == 0) F.gateTok = 1;   // (the word starts at 0)
-        hipLaunchKernelGGL(k_gate_signal, dim3(1), dim3(64), 0, sb, F.gate, F.gateTok);
+        if (inject != 2)   // (2: the token is withheld -- tests of the timeout)
+            hipLaunchKernelGGL(k_gate_signal, dim3(1), dim3(64), 0, sb, F.gate, F.gateTok);
         hipLaunchKernelGGL(k_gate_wait, dim3(1), dim3(64), 0, sa, (const u32*)F.gate, F.gateTok, (const u32*)S.dplan,
-                           F.gplan, S.derr);
+                           F.gplan);
         NR_CHECK(hipGetLastError());
         visPlan = F.gplan;
     } else if (sb != sa) {
@@ -2252,7 +2342,8 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (S.nitems > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = ext_stop() && !e1;
-        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan}, std::min<u32>(S.nitems, 8192), sa,
+        const WarmCheck wc{wstat, tag, (epoch + 1) * S.pairs, sc.dfail};
+        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa,
                        vs ? F.evVis : nullptr, owned_share_large(fp.period, fp.mask, bp.src.n), zmode,
                        fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
@@ -2318,11 +2409,8 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         sc.lastSplit = tb->knownSplit;
     }
     // warm: the schedule kept from this buffer's last validated binning under this key
+    warm_poll(ctx);
     if (!ordered && !exact && sched_matches(sc, tb, key)) {
-        if (sc.sched.herr && *(volatile u32*)sc.sched.herr)
-            nr_set_error_msg(*(volatile u32*)sc.sched.herr == 2
-                                 ? "triangle batch: a raster's wait for its warm binning timed out (NR_GATE)"
-                                 : "triangle batch: a warm binning found a tile over its kept range");
         if (warm_enqueue(ctx, fp, bp, tb)) {
             ctx->lastPath = 1;
             ++sc.warmBatches;
@@ -2386,6 +2474,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
 // entry point that enqueues work on, or reads, the context's buffers, so the
 // re-run is ordered before anything that depends on the batch.
 void settle(RenderContext* ctx) {
+    warm_poll(ctx);
     PendingBatch* pb = reinterpret_cast<PendingBatch*>(ctx->pendingBatch);
     if (!pb) return;
     ctx->pendingBatch = nullptr;

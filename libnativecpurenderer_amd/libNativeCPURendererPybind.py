@@ -441,6 +441,15 @@ class RenderContext:
     def warm_batch_count(self) -> int:
         return lib.GetWarmBatchCount(self._ptr)
 
+    def set_warm_fault_injection(self, mode: int):
+        """Testing: a fault in the next warm batch (1 tile ranges overflow, 2
+        the binning's token is withheld, 3 a workgroup's pairs are dropped);
+        the frame must stay exact and the failure be latched."""
+        lib.SetWarmFaultInjection(self._ptr, int(mode))
+
+    def warm_failure_count(self) -> int:
+        return lib.GetWarmFailureCount(self._ptr)
+
     def set_force_ordered_raster(self, on: bool = True):
         lib.SetForceOrderedRaster(self._ptr, on)
 

@@ -1,0 +1,114 @@
+"""Warm binning (a TriangleBuffer drawn again under the binning key of its last
+validated binning, k_bin_warm) against the CPU oracle, frame by frame, and its
+checks: a warm batch whose binning fails (a tile over its kept range, pairs
+missing, the binning's token never arriving) must still give the exact frame
+(k_vis WarmCheck fallback) and latch the failure.
+
+Geometry with off-screen clusters of huge-coordinate slivers: the cold count
+bins a triangle with a screen coordinate beyond 1e7 into every column of its
+rows (tri_tiles), so the warm binning's cluster cull must not drop such a
+cluster by x.  Several frames per context, so every binning
+set runs more than one epoch of its cursors."""
+import numpy as np
+import pytest
+
+import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _huge_cluster(rng, n=64):
+    """64 triangles left of the screen (x in [-100, -50]); the first is a tall
+    sliver spanning y = +-2e7 (binned full-width by the cold count)."""
+    xy = np.empty((n, 6))
+    for t in range(n):
+        cx, cy = rng.uniform(-100, -50), rng.uniform(0, 400)
+        xy[t] = [cx, cy, cx + 3, cy + 1, cx + 1, cy + 4]
+    xy[0] = [-100.0, -2e7, -50.0, 2e7, -60.0, 0.0]
+    z = rng.uniform(0, 1, size=(n, 3))
+    c = rng.uniform(0, 1, size=(n, 12))
+    c[:, 3::4] = 1.0
+    return xy, z, c
+
+
+def _scene(W, H, mesh_rc=(60, 200)):
+    rng = np.random.default_rng(5)
+    mesh = scenes.sphere_mesh(W, H, *mesh_rc)
+    off1 = _huge_cluster(rng)
+    off2 = _huge_cluster(rng)
+    off2[0][:, 0::2] += W + 160.0   # right of the screen
+    parts = [off1, mesh, off2]   # clusters of 64: the mesh starts at triangle 64
+    pad = (-len(mesh[0])) % 64   # keep the second huge cluster aligned to a cluster boundary
+    if pad:
+        parts[1] = tuple(a[:len(a) - pad] for a in mesh)
+    return tuple(np.ascontiguousarray(np.concatenate([p[k] for p in parts])) for k in range(3))
+
+
+def _owned(H, n, r):
+    from libnativecpurenderer_amd import sharding
+    return sharding.owned_rows(H, n, r)
+
+
+def _frames(fac, W, H, scene, nframes, shard=None, inject=None):
+    xy, z, c = scene
+    ctx = fac.context(W, H, False)
+    if fac.name == "gpu":
+        from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+        ctx.set_warm_binning(1)
+        if shard is not None:
+            ctx.set_shard(*shard)
+        buf = R.TriangleBuffer(xy, c, z=z, gouraud=True)
+    outs = []
+    for k in range(nframes):
+        if inject is not None and fac.name == "gpu" and k == inject[0]:
+            ctx.set_warm_fault_injection(inject[1])
+        ctx.set_color(0.1, 0.2, 0.3, 0.3 if k % 2 else 0.1)   # (non-uniform every other frame)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        if fac.name == "gpu":
+            ctx.draw_triangle_buffer(buf)
+        else:
+            ctx.draw_triangles(xy, c, z=z)
+        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+    return outs, ctx
+
+
+@pytest.mark.parametrize("shard", [None, (2, 0), (2, 1), (8, 3)])
+def test_warm_frames_with_huge_offscreen_clusters(gpu, oracle, shard):
+    W, H = 640, 400
+    scene = _scene(W, H)
+    want, _ = _frames(oracle, W, H, scene, 8)
+    got, ctx = _frames(gpu, W, H, scene, 8, shard=shard)
+    rows = slice(None) if shard is None else _owned(H, *shard)
+    for k, (g, o) in enumerate(zip(got, want)):
+        assert scenes.bits_equal(g["f64"][rows], o["f64"][rows]), f"frame {k}: {scenes.first_mismatch(g['f64'][rows], o['f64'][rows])}"
+        assert np.array_equal(g["depth"][rows], o["depth"][rows]), f"frame {k} depth"
+    assert ctx.warm_batch_count() >= 5, ctx.warm_batch_count()   # frames 2..7 after the first validated draw
+    assert ctx.warm_failure_count() == 0
+
+
+@pytest.mark.parametrize("mode,mesh_rc", [(1, (60, 200)), (2, (60, 200)), (3, (60, 200)),
+                                          (1, (250, 700)), (3, (250, 700))])
+def test_warm_fault_falls_back_exactly(gpu, oracle, mode, mesh_rc):
+    """A fault injected into the 4th frame's warm batch (1 ranges overflow, 2
+    token withheld -- only on the beside-raster path of small batches, 3 a
+    workgroup's pairs dropped; 350k triangles bin inline): every frame still
+    equals the oracle's, the failure is counted and its message latched, and
+    the next frames bin cold (1, 3: the buffer is banned from warm binning) or
+    warm again after a new cold binning (2)."""
+    from libnativecpurenderer_amd import _lib
+    W, H = 640, 400
+    scene = _scene(W, H, mesh_rc)
+    want, _ = _frames(oracle, W, H, scene, 7)
+    _lib.clear_last_error()
+    got, ctx = _frames(gpu, W, H, scene, 7, inject=(3, mode))
+    for k, (g, o) in enumerate(zip(got, want)):
+        assert scenes.bits_equal(g["f64"], o["f64"]), f"frame {k}: {scenes.first_mismatch(g['f64'], o['f64'])}"
+        assert np.array_equal(g["depth"], o["depth"]), f"frame {k} depth"
+    assert ctx.warm_failure_count() == 1
+    assert "warm binning" in _lib.last_error(), _lib.last_error()
+    nwarm = ctx.warm_batch_count()
+    if mode == 2:
+        assert nwarm >= 4, nwarm   # frames 1-3, and 5-6 once re-captured
+    else:
+        assert nwarm == 3, nwarm   # frames 1-3 only: the buffer bins cold after the failure

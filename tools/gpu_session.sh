@@ -7,6 +7,7 @@
 #   bench[:ARGS]    python bench.py ARGS  (ARGS: comma-separated, e.g. bench:--config,c2,--steps,20)
 #   trace[:ARGS]    rocprofv3 --kernel-trace --hip-runtime-trace of bench.py ARGS (+ timeline.py)
 #   ktrace[:ARGS]   rocprofv3 --kernel-trace of bench.py ARGS (+ timeline.py), no runtime trace
+#   ctrace[:ARGS]   rocprofv3 --kernel-trace --memory-copy-trace of bench.py ARGS
 #   stats[:ARGS]    rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   ab:ENV1%ENV2%.. bench lines under each environment (ENVk = A=1+B=2), twice, interleaved; BENCH_ARGS env for the bench flags
 #   py:SCRIPT,ARGS  python SCRIPT ARGS
@@ -46,6 +47,8 @@ for step in "$@"; do
            run ktrace 600 rocprofv3 --kernel-trace -d "$d" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra "${A[@]}"
            kt=$(find "$d" -name '*kernel_trace.csv' | head -1)
            [ -n "$kt" ] && python3 tools/timeline.py "$kt" 4 > "$OUT/$(printf %02d $i)_timeline.txt" 2>&1 ;;
+    ctrace) d="$OUT/ctrace$i"   # kernel + memory-copy trace (no runtime trace, no counters)
+           run ctrace 600 rocprofv3 --kernel-trace --memory-copy-trace -d "$d" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra "${A[@]}" ;;
     stats) d="$OUT/stats$i"
            run stats 600 rocprofv3 --kernel-trace --stats -d "$d" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extra "${A[@]}" ;;
     ab)    IFS='%' read -r -a ENVS <<< "$arg"
