@@ -94,9 +94,7 @@ def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True, frame_out="rgb"):
 EVENT_EVERY = 10   # timed-region frames per HIP-event-timed frame of the dominant kernel (each record pair
                    # perturbs the stream: 1 in 4 cost ~7 % of C3 throughput, 1 in 10 ~2 %)
 
-KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)",
-                 "gvis_raster": "k_gvis_raster (whole-frame visibility buffer)",
-                 "gvis_resolve": "k_gvis_resolve (whole-frame visibility buffer)"}
+KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)"}
 
 
 def kernel_bytes(cfg, n_tri, path, frac=1.0, frame_out="rgb"):
@@ -104,17 +102,7 @@ def kernel_bytes(cfg, n_tri, path, frac=1.0, frame_out="rgb"):
     The tiled rasterisers read each triangle (positions, depths, colours) once
     and write the framebuffer and depth once, all inside one kernel (k_vis
     shades its tiles itself; k_tile_raster keeps the tile in registers); k_vis
-    also writes the u8 frame (k_to_u8_rows does it after the ordered raster).
-    The whole-frame visibility buffer splits the same bytes over two kernels:
-    k_gvis_raster reads every triangle's positions and depths (48 + 24 B; a
-    rank cannot know which triangles fall in its rows without reading them),
-    k_gvis_resolve the colours (96 B Gouraud / 32 B flat, the owned share) and
-    writes the owned framebuffer, depth and frame output."""
-    if path == "order-free-frame":
-        s_col = 96 if cfg["gouraud"] else 32
-        out = FRAME_OUT_BPP[frame_out]
-        return {"gvis_raster": int(n_tri * 72),
-                "gvis_resolve": int(frac * (n_tri * s_col + cfg["W"] * cfg["H"] * (8 * 3 + 4 + out)))}
+    also writes the u8 frame (k_to_u8_rows does it after the ordered raster)."""
     return {"tile_raster": algorithmic_bytes(cfg, n_tri, frac, u8=(path == "order-free"), frame_out=frame_out)}
 
 
@@ -305,7 +293,7 @@ class Runner:
         self.drain()
 
         names = ("tri_count", "tri_scan", "tri_emit", "tri_sort", "tile_ranges", "vis_init", "tile_raster",
-                 "gvis_raster", "gvis_resolve", "resolve", "fill", "output", "gather")
+                 "resolve", "fill", "output", "gather")
         # (1) breakdown pass: HIP events around every kernel (they add launch
         #     gaps, so this pass is not the headline)
         ctx.reset_kernel_timing()
@@ -349,21 +337,13 @@ class Runner:
         dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
         achieved = kb[dom] / (dom_us * 1e-6) / 1e9
         B = algorithmic_bytes(self.cfg, self.n_tri, frame_out=self.frame_output)   # whole frame
-        ksym = {"gvis_raster": "k_gvis_raster", "gvis_resolve": "k_gvis_resolve"}.get(
-            dom, "k_tile_raster" if path == "ordered" else "k_vis")
+        ksym = "k_tile_raster" if path == "ordered" else "k_vis"
         traffic, traffic_src = load_pmc_traffic(self.cfg_name, self.nsh if self.world == 1 else 1,
                                                 slots if self.world == 1 else None, self.frame_output, ksym)
         if self.world > 1:
             traffic, traffic_src = None, None   # per-rank PMC passes are not taken on multi-GPU runs
-        path_extra = {}
-        if len(kb) > 1:   # the whole-frame visibility buffer: both kernels' bytes over both kernels' times
-            tot_b = sum(kb.values())
-            tot_us = sum(kernels.get(k, 0.0) for k in kb)
-            if tot_us > 0:
-                path_extra = {"path_kernels": {k: {"us": kernels.get(k), "algorithmic_bytes": kb[k]} for k in kb},
-                              "path_frac": round(tot_b / (tot_us * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4)}
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic, **path_extra,
+                "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
                 "traffic_source": traffic_src or "none for this config/share (null)",
                 "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
                 "algorithmic_bytes_per_launch": kb[dom], "rank_share_of_frame": round(share, 6),
@@ -410,6 +390,8 @@ def main():
                          "overlapped with frame k+1), as the video caller (PutRendererContextFrame) needs it")
     ap.add_argument("--no-kernel-timing", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
+    ap.add_argument("--lib", default=None,
+                    help="experiment: load another build of the library (tools/exp A/B and probe builds)")
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="experiment: render shard 0 of N on this one GPU (no gather) to time one rank's share")
     ap.add_argument("--gloo-test", action="store_true",
@@ -424,6 +406,9 @@ def main():
                          "fastest -- the root also receives every other rank's bands, so it gets less to render "
                          "when the gather dominates")
     args = ap.parse_args()
+    if args.lib:
+        from libnativecpurenderer_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(args.lib)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -150,7 +150,6 @@ i64 GetLastRasterPath(RenderContext* ctx);                               /* NEW:
 void SetForceOrderedRaster(RenderContext* ctx, bool on);                 /* NEW: A/B and tests */
 void SetPairCapacityOverride(RenderContext* ctx, i64 pairs);             /* NEW: tests (0 = automatic) */
 void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW: k_vis variant 0 auto, 1 coop, 2 lane-only */
-void SetFrameVisRaster(RenderContext* ctx, i64 mode);                    /* NEW: frame visibility buffer 0 auto, 1 on, 2 off */
 void SetWarmBinning(RenderContext* ctx, i64 mode);                       /* NEW: one-pass binning of a repeat draw 0 auto, 1 on, 2 off */
 i64 GetWarmBatchCount(RenderContext* ctx);                               /* NEW (testing): batches binned warm */
 void SetWarmFaultInjection(RenderContext* ctx, i64 mode);                /* NEW (testing): fault in the next warm batch

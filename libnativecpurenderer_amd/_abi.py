@@ -82,7 +82,6 @@ DEVICE_ABI = {
     "SetForceOrderedRaster": (None, (P, B)),
     "SetPairCapacityOverride": (None, (P, L)),
     "SetCoopRaster": (None, (P, L)),
-    "SetFrameVisRaster": (None, (P, L)),
     "SetWarmBinning": (None, (P, L)),
     "GetWarmBatchCount": (L, (P,)),
     "SetWarmFaultInjection": (None, (P, L)),

@@ -8,8 +8,7 @@ import os
 
 from . import _abi
 
-# NR_LIB: another build of the same library (A/B and check builds under tools/exp only)
-LIB_PATH = os.environ.get("NR_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libNativeCPURenderer.so")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libNativeCPURenderer.so")
 
 _lib = None
 

@@ -51,19 +51,9 @@ void ClearLastError() {
 // contexts and textures of that device, so cross-object ordering (texture
 // uploads, render-to-texture) is the reference's single-threaded order.
 // ---------------------------------------------------------------------------
-#ifndef NR_MAIN_PRIO
-#define NR_MAIN_PRIO 1   // main stream at the greatest priority
-#endif
-// Stream priorities (NR_STREAM_PRIO): 0 main stream above the binning
-// stream, 1 binning above main, 2 both at the least priority.
-static int stream_prio_mode() {
-    static const int v = [] {
-        const char* e = getenv("NR_STREAM_PRIO");
-        const int x = e ? atoi(e) : -1;
-        return x >= 0 && x <= 2 ? x : 0;
-    }();
-    return v;
-}
+// Stream priorities: the main stream at the greatest, the binning stream at
+// the least (the next batch's binning fills the gaps the current raster
+// leaves instead of competing with it).
 static std::mutex g_dev_mu;
 static std::vector<hipStream_t> g_streams;
 
@@ -75,7 +65,7 @@ hipStream_t nr_stream_for(int device) {
         int least = 0, greatest = 0;
         NR_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
         NR_CHECK(hipStreamCreateWithPriority(&g_streams[device], hipStreamNonBlocking,
-                                             stream_prio_mode() == 0 && NR_MAIN_PRIO ? greatest : least));
+                                             greatest));
     }
     return g_streams[device];
 }
@@ -85,13 +75,11 @@ hipStream_t nr_bin_stream_for(int device) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     if ((int)g_bin_streams.size() <= device) g_bin_streams.resize(device + 1, nullptr);
     if (!g_bin_streams[device]) {
-        // lowest priority: the next batch's binning fills the gaps the
-        // current raster leaves instead of competing with it
         NR_CHECK(hipSetDevice(device));
         int least = 0, greatest = 0;
         NR_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
         NR_CHECK(hipStreamCreateWithPriority(&g_bin_streams[device], hipStreamNonBlocking,
-                                             stream_prio_mode() == 1 ? greatest : least));
+                                             least));
     }
     return g_bin_streams[device];
 }
@@ -309,8 +297,7 @@ static void timing_collect(RenderContext* ctx) {
 
 static const char* kKernelNames[NRK_COUNT_] = {"tri_count", "tri_scan",    "tri_emit", "tri_sort",
                                                "tile_ranges", "tile_raster", "prim",     "fill",
-                                               "resolve",   "vis_init",    "output",   "gather",
-                                               "gvis_raster", "gvis_resolve"};
+                                               "resolve",   "vis_init",    "output",   "gather"};
 
 extern "C" {
 
@@ -367,7 +354,7 @@ void DestroyRenderContext(RenderContext* ctx) {
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
                     t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
-                    t.fdone,     t.kslot, t.orec, t.gkey};
+                    t.fdone,     t.kslot, t.orec};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     for (auto& F : t.fset) {

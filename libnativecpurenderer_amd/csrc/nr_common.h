@@ -89,13 +89,6 @@ struct TriScratch {
     int coopMode = 0;                       // k_vis variant: 0 auto, 1 coop, 2 lane-only (SetCoopRaster)
     u32 splitAt = 0, dslice = 0;            // dense-tile split limits (SetSplitLimits; 0: NR_SPLIT_AT / NR_DSLICE)
     f64* stage = nullptr; size_t stage_cap = 0;   // DrawTriangles() with host arrays
-    // whole-frame visibility buffer (nr_tri_gvis.hip): W*H packed keys; state 1:
-    // every key of the owned rows of (gkeyW, gkeyH, gkeyPeriod, gkeyMask) is
-    // gkeyInit << 32; 0: unknown (the next batch initialises them)
-    u64* gkey = nullptr; size_t gkey_cap = 0;
-    int gkeyState = 0; u32 gkeyInit = 0;
-    i64 gkeyW = 0, gkeyH = 0; int gkeyPeriod = 0; u64 gkeyMask = 0;
-    int gvisMode = 0;                       // 0 automatic (NR_GVIS), 1 always, 2 never (SetFrameVisRaster)
     // warm binning (nr_tri_free.hip): the tile offsets, k_vis work items and
     // plan totals of the last validated binning of one TriangleBuffer under
     // one binning key -- a later draw of the same buffer under the same key
@@ -131,12 +124,11 @@ struct TriScratch {
     u64 warmFailures = 0;                   // warm batches that failed their checks (GetWarmFailureCount)
     std::vector<u64> warmBanned;            // buffers (uid) whose warm binning failed a check: binned cold
     int warmInject = 0;                     // testing: fault injected into the next warm batch (SetWarmFaultInjection)
-    f64 srcMeanArea = -1;                   // mean |signed area| of the batch being drawn, user space (-1: unknown)
 };
 
 enum NRKernelId { NRK_TRI_COUNT = 0, NRK_TRI_SCAN, NRK_TRI_EMIT, NRK_TRI_SORT, NRK_TILE_RANGES,
                   NRK_TILE_RASTER, NRK_PRIM, NRK_FILL, NRK_RESOLVE, NRK_VIS_INIT, NRK_OUTPUT, NRK_GATHER,
-                  NRK_GV_RASTER, NRK_GV_RESOLVE, NRK_COUNT_ };
+                  NRK_COUNT_ };
 
 struct RenderContext {
     i64 width = 0, height = 0;
@@ -225,7 +217,6 @@ struct TriangleBuffer {
     bool known = false;
     BinKey knownKey;
     u32 knownPairs = 0, knownHeavy = 0, knownItems = 0, knownSplit = 0;
-    f64 meanArea = -1;    // mean |signed area| of the triangles in user space (computed at upload)
     u64 uid = 0;          // process-unique id (a context's warm schedule names its buffer by it)
     // per cluster of CLUSTER consecutive triangles (one wave of the binning
     // kernels): its user-space bounding box {xmin, ymin, xmax, ymax} (NaN when

@@ -359,16 +359,10 @@ struct FrameParams {
 // Y of every pixel, U and V from the even pixel of each 2x2 block (tiles have
 // even sizes and origins, so a block never straddles two).
 // Output stores of the rasters' shading passes (framebuffer, depth, frame
-// output): written once per frame and not read again by the kernel.
-// NR_NT_STORE=1: non-temporal (streaming) stores (A/B).
-#ifndef NR_NT_STORE
-#define NR_NT_STORE 0
-#endif
+// output): written once per frame and not read again by the kernel (plain
+// stores; non-temporal ones were not faster, round 3).
 template <class T>
-__device__ __forceinline__ void out_store(T* p, T v) {
-    if (NR_NT_STORE) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+__device__ __forceinline__ void out_store(T* p, T v) { *p = v; }
 __device__ __forceinline__ void store_frame_out(const FrameParams& fp, i64 p, i64 px, i64 py, f64 cr, f64 cg, f64 cb,
                                                 f64 ca) {
     if (!fp.frameU8) return;
@@ -487,11 +481,6 @@ void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* of
 // so the batch is sized exactly in the call -- an overflow re-run never reads
 // them after it returns
 void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned, bool ordered = false);
-// the whole-frame visibility buffer (nr_tri_gvis.hip) for opaque Z LESS + write
-// batches of small triangles: chosen per batch by gvis_wanted (objMeanArea: the
-// batch's mean |signed area| in user space, < 0 unknown)
-bool gvis_wanted(const RenderContext* ctx, const TriSrc& src, f64 objMeanArea);
-void draw_gvis(RenderContext* ctx, const TriSrc& src, const FrameParams& fp, const BinParams& bp);
 void settle(RenderContext* ctx);
 
 }  // namespace nrtri

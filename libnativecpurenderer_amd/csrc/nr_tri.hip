@@ -79,19 +79,6 @@ void finish_batch(RenderContext* ctx, const FrameParams& fp) {
 
 namespace {
 
-// Mean |signed area| of the triangles (user space; non-finite ones skipped):
-// picks the whole-frame visibility buffer for meshes of small triangles.
-f64 host_mean_area(const f64* xy, i64 n) {
-    f64 sum = 0;
-    i64 cnt = 0;
-    for (i64 t = 0; t < n; ++t) {
-        const f64* p = xy + t * 6;
-        const f64 a = fabs((p[2] - p[0]) * (p[5] - p[1]) - (p[4] - p[0]) * (p[3] - p[1])) * 0.5;
-        if (a < 1e300) { sum += a; ++cnt; }
-    }
-    return cnt ? sum / (f64)cnt : -1.0;
-}
-
 // User-space bounding boxes of the NR_CLUSTER-triangle clusters (TriangleBuffer::cbox).
 std::vector<f64> host_cluster_boxes(const f64* xy, i64 n) {
     const i64 nc = (n + NR_CLUSTER - 1) / NR_CLUSTER;
@@ -152,10 +139,9 @@ Opacity device_opacity(RenderContext* ctx, const TriSrc& src) {
 }
 
 void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 n, bool gouraud, Opacity opq,
-          TriangleBuffer* tb = nullptr, bool callerOwned = false, f64 meanArea = -1) {
+          TriangleBuffer* tb = nullptr, bool callerOwned = false) {
     NR_CHECK(hipSetDevice(ctx->device));
     settle(ctx);
-    ctx->tri.srcMeanArea = meanArea;
     if (n <= 0 || ctx->width <= 0 || ctx->height <= 0) return;
     if (!ctx->depthTest) nr_materialize_depth(ctx);
     TriSrc src{xy, z, rgba, gouraud ? 1 : 0, n};
@@ -245,8 +231,7 @@ void DrawTriangles(RenderContext* ctx, const f64* xy, const f64* z, const f64* r
     if (z) NR_CHECK(hipMemcpyAsync(dz, z, (size_t)n * 3 * sizeof(f64), hipMemcpyHostToDevice, ctx->stream));
     NR_CHECK(hipMemcpyAsync(dc, rgba, (size_t)n * ncol * sizeof(f64), hipMemcpyHostToDevice, ctx->stream));
     NR_CHECK(hipStreamSynchronize(ctx->stream));   // caller may reuse its arrays on return
-    draw(ctx, dxy, z ? dz : nullptr, dc, n, gouraud, host_opacity(rgba, n, gouraud), nullptr, false,
-         host_mean_area(xy, n));
+    draw(ctx, dxy, z ? dz : nullptr, dc, n, gouraud, host_opacity(rgba, n, gouraud), nullptr, false);
 }
 
 // New: a device-resident triangle soup (the H2D point; drawn many times).
@@ -257,7 +242,6 @@ TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f
     tb->n = n;
     tb->gouraud = gouraud;
     tb->opaque = n > 0 && host_opacity(rgba, n, gouraud) == OPQ_OPAQUE;
-    tb->meanArea = n > 0 ? host_mean_area(xy, n) : -1.0;
     std::vector<f64> cb;
     if (n > 0) cb = host_cluster_boxes(xy, n);
     NR_CHECK(hipGetDevice(&tb->device));
@@ -299,8 +283,7 @@ i64 GetTriangleBufferCount(TriangleBuffer* tb) { return tb->n; }
 
 void DrawTriangleBuffer(RenderContext* ctx, TriangleBuffer* tb) {
     // a TriangleBuffer never changes: its binning may overlap the previous batch's raster
-    draw(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud, tb->opaque ? OPQ_OPAQUE : OPQ_BLENDED, tb, false,
-         tb->meanArea);
+    draw(ctx, tb->xy, tb->z, tb->rgba, tb->n, tb->gouraud, tb->opaque ? OPQ_OPAQUE : OPQ_BLENDED, tb, false);
 }
 
 // New: count covered on-screen pixel x triangle pairs (the "shaded+Z-tested
@@ -315,7 +298,7 @@ i64 GetFragmentCount(RenderContext* ctx) { return (i64)ctx->fragTotal; }
 // New (testing / A-B measurement): the whole-frame visibility buffer for
 // opaque Z LESS + write batches, 0 automatic (small triangles, NR_GVIS), 1
 // every such batch, 2 never (the tiled k_vis path).
-void SetFrameVisRaster(RenderContext* ctx, i64 mode) { ctx->tri.gvisMode = (int)(mode >= 0 && mode <= 2 ? mode : 0); }
+
 
 // New (testing / A-B measurement): warm binning of a TriangleBuffer drawn
 // again under the key of its last validated binning (one binning pass into

@@ -69,31 +69,20 @@ __device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, in
 #define NR_PROBE_STAMP(k) do { } while (0)
 #endif
 
-#ifndef NR_VWG
-#define NR_VWG 256
-#endif
+constexpr int VWG = 256;  // k_vis workgroup
 // k_vis occupancy: 4 waves per SIMD (<= 128 VGPRs, and LDS <= 40 KB per
-// workgroup: 280 shading records over the keys + NR_REC_EXTRA) measured 6-10 %
+// workgroup: 280 shading records over the keys + REC_EXTRA) measured 6-10 %
 // faster on C3 than 3 (135 VGPRs, 53.5 KB); k_vis is latency-bound.
-#ifndef NR_VIS_WAVES_PER_EU
-#define NR_VIS_WAVES_PER_EU 4
-#endif
-constexpr int VWG = NR_VWG;  // k_vis workgroup
-#ifndef NR_SLICE
-#define NR_SLICE 1024
-#endif
-constexpr u32 SLICE = NR_SLICE;   // longest work item (triangles)
-#ifndef NR_SLICE_MIN
-#define NR_SLICE_MIN 64
-#endif
-constexpr u32 SLICE_MIN = NR_SLICE_MIN;   // shortest slice of a split tile
-#ifndef NR_SLICE_TARGET
-#define NR_SLICE_TARGET 256   // round 4: 512 -> 256 (an 8-way share's slices 512 -> 1024: 0.046 -> 0.041 ms per frame)
-#endif
-#ifndef NR_TPT
-#define NR_TPT 4
-#endif
-constexpr int TPT = NR_TPT;   // triangles per thread in the binning kernels
+constexpr int VIS_WPE = 4;
+constexpr u32 SLICE = 1024;      // longest work item (triangles)
+constexpr u32 SLICE_MIN = 64;    // shortest slice of a split tile
+// Items the plan kernel aims for when it picks the slice length.  Round 4
+// (warm binning, spill-free k_vis): 256, i.e. slices of 1024 for every batch of
+// >= 2^17 owned pairs.  An 8-way C3 share (~150k pairs) used to get slices of
+// 512: its split tiles' slot merges cost more than the longer slices (0.046 ->
+// 0.041 ms per frame, C2 -1 %, C3 unchanged; profiles/r04/ab_slice_target.txt).
+constexpr u32 SLICE_TARGET = 256;
+constexpr int TPT = 4;   // triangles per thread in the binning kernels (2 / 8 measured slower, round 4)
 constexpr int LDS_HIST_MAX = 16384;
 
 // Tile rectangle of a triangle, packed for the emit pass (16 bits per bound;
@@ -224,23 +213,18 @@ constexpr u32 HEAVY_PAIRS = 256;   // a dense tile (for the k_vis workgroup-size
 // slice merges the others' keys and shades the tile, the kernel's longest
 // chain (a 16-slice 1080p tile started 62 us into a 98 us raster,
 // tools/exp/probe_items.py).
-// One-slice classes are PLAN_ONE equal bins of [1, lim] (NR_CLASS_LIN=0:
-// octaves, which left a C3 frame's items -- nearly all in [256, 1024] -- in
-// two classes, in tile order within each): C3 -0.8 %, 1M tris at 1080p -1.3 %,
+// One-slice classes are PLAN_ONE equal bins of [1, lim] (octaves had left a
+// C3 frame's items -- nearly all in [256, 1024] -- in two classes, in tile
+// order within each): C3 -0.8 %, 1M tris at 1080p -1.3 %,
 // C2 -2 % per frame (profiles/r03_c3/ab_class_lin.txt).
 constexpr int PLAN_ONE = 10, PLAN_SPLIT = 3, PLAN_NB = 1 + PLAN_ONE + PLAN_SPLIT;
-#ifndef NR_CLASS_LIN
-#define NR_CLASS_LIN 1
-#endif
 __device__ __forceinline__ int size_class(u32 c, u32 lim, u32 dsl) {
     if (c > lim) {
         const u32 ni = (c + dsl - 1) / dsl;
         return PLAN_NB - (ni >= 8 ? 1 : ni >= 4 ? 2 : 3);
     }
     if (c == 0) return 0;
-    if (NR_CLASS_LIN) return 1 + min((int)((float)c * ((float)PLAN_ONE / (float)(lim + 1))), PLAN_ONE - 1);
-    const int l = 31 - __clz(c);
-    return 1 + (l < PLAN_ONE - 1 ? l : PLAN_ONE - 1);
+    return 1 + min((int)((float)c * ((float)PLAN_ONE / (float)(lim + 1))), PLAN_ONE - 1);
 }
 
 // Tiles are taken PLAN_T at a time (thread = tile: coalesced), each round a
@@ -601,27 +585,13 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
     }
 }
 
-// NR_PLAN_REG=0 keeps the multi-round plan kernels (A/B).
-static bool plan_reg() {
-    static const bool v = [] {
-        const char* e = getenv("NR_PLAN_REG");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
 // Which plan kernel: the 256-thread one when the batch's owned share is large
 // (>= 2^17 triangles' worth: C3 unsharded 0.167 -> 0.160 ms per frame, C3 4-way
 // share 0.0654 -> 0.0627 ms; the plan runs beside the previous, long k_vis),
 // the 1024-thread one otherwise: a short k_vis leaves the plan mostly alone and
 // the wider workgroup is faster (C3 8-way share 0.0535 -> 0.0516 ms; C2, 10k
-// triangles, 0.0802 -> 0.069 ms).  NR_PLAN_SMALL=0/1 forces one (A/B).
+// triangles, 0.0802 -> 0.069 ms).
 static bool owned_share_large(int period, u64 mask, i64 ntri) {
-    static const int v = [] {
-        const char* e = getenv("NR_PLAN_SMALL");
-        return e ? atoi(e) : -1;
-    }();
-    if (v >= 0) return v != 0;
     const u64 m = period >= 64 ? mask : (mask & ((1ull << period) - 1ull));
     const f64 share = period == 1 ? 1.0 : (f64)__builtin_popcountll(m) / (f64)period;
     return (f64)ntri * share >= (f64)(1 << 17);
@@ -759,17 +729,6 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     // this wave's cluster of each of its TPT triangle groups (NR_CLUSTER == 64:
     // one wave, so the test and the skip are wave-uniform)
     static_assert(NR_CLUSTER == 64, "a cluster is one wave's triangles");
-#ifndef NR_BIN_PREFETCH
-#define NR_BIN_PREFETCH 0   // 1: the positions are loaded before the cluster test (one latency round less, all bytes)
-#endif
-    f64 pxy[TPT][6];
-    if (NR_BIN_PREFETCH) {
-#pragma unroll
-        for (int k = 0; k < TPT; ++k) {
-            const i64 t = base + k * 256 + tid;
-            if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
-        }
-    }
     bool cl[TPT];
     bool anyc = false;
 #pragma unroll
@@ -781,17 +740,14 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     // a workgroup none of whose clusters reaches an owned tile has nothing to do
     // (most of them on a sharded frame's rank)
     if (cbox && !__syncthreads_or(anyc ? 1 : 0)) return;
-#ifndef NR_BIN_STOP
-#define NR_BIN_STOP 0   // timing probe builds only: 1/2/3 stop after the cluster test / the histogram / the reservation
-#endif
-    if (NR_BIN_STOP == 1) return;
     if (tid == 0) wgPairs = 0;
-    if (!NR_BIN_PREFETCH) {
+    // (loading the positions before the cluster test -- one latency round
+    // less, all bytes -- was not faster, round 4)
+    f64 pxy[TPT][6];
 #pragma unroll
-        for (int k = 0; k < TPT; ++k) {
-            const i64 t = base + k * 256 + tid;
-            if (cl[k] && t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
-        }
+    for (int k = 0; k < TPT; ++k) {
+        const i64 t = base + k * 256 + tid;
+        if (cl[k] && t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
     }
     if (LDSH) for (int b = tid; b < hbins; b += 256) hist[b] = 0;
     __syncthreads();   // (hist and wgPairs zeroed)
@@ -816,12 +772,9 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
             for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[hrow + tx], 1u);
         }
     }
-    if (NR_BIN_STOP == 2) return;
     {   // the workgroup's pair total (one global atomic)
-        u32 wp = myPairs;
-        wp += __shfl_xor(wp, 32); wp += __shfl_xor(wp, 16); wp += __shfl_xor(wp, 8);
-        wp += __shfl_xor(wp, 4); wp += __shfl_xor(wp, 2); wp += __shfl_xor(wp, 1);
-        if ((tid & 63) == 0 && wp) atomicAdd(&wgPairs, wp);
+        const u32 wp = wave_scan(myPairs, tid & 63);
+        if ((tid & 63) == 63 && wp) atomicAdd(&wgPairs, wp);
     }
     if (LDSH) {
         __syncthreads();
@@ -841,7 +794,6 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     }
     __syncthreads();   // (LDS ranges reserved; wgPairs complete)
     if (tid == 0 && wgPairs) atomicAdd(&wstat[WS_SUM], wgPairs);
-    if (NR_BIN_STOP == 3) return;
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
@@ -891,27 +843,11 @@ __device__ __forceinline__ int opaque_tid() {
 // turned into a shading record in LDS, and the pixels are then shaded from
 // LDS.  Per-pixel dependent global loads (eight rounds of latency per
 // thread) were the largest cost of the fused raster.
-#ifndef NR_HTS
-#define NR_HTS 512
-#endif
-#ifndef NR_REC_EXTRA   // LDS beyond the keys for shading records (k_vis stays <= 40 KB: 4 workgroups per CU)
-#define NR_REC_EXTRA 19200
-#endif
-constexpr int HTS = NR_HTS;    // hash slots (power of two)
-#ifndef NR_HTS_WIDE
-#define NR_HTS_WIDE 1024   // hash slots of the 512-thread instance (its LDS holds two workgroups per CU)
-#endif
-#ifndef NR_HTS3
-#define NR_HTS3 1024   // hash slots of the 3-wave instance (its LDS may grow to a third of the CU's)
-#endif
-#ifndef NR_MAXPROBE
-#define NR_MAXPROBE 16
-#endif
-constexpr int MAXPROBE = NR_MAXPROBE;   // linear-probe limit: a winner not placed / found within it loads directly
-#ifndef NR_OVF_Q
-#define NR_OVF_Q 1
-#endif
-constexpr int OVF_Q = NR_OVF_Q;   // directly loaded records in flight per thread (0: one at a time, in pass 3)
+constexpr int REC_EXTRA = 19200;   // LDS beyond the keys for shading records (k_vis stays <= 40 KB: 4 workgroups per CU)
+constexpr int HTS = 512;           // hash slots (power of two)
+constexpr int HTS_WIDE = 1024;     // hash slots of the 512-thread instance (its LDS holds two workgroups per CU)
+constexpr int MAXPROBE = 16;       // linear-probe limit: a winner not placed / found within it loads directly
+constexpr int OVF_Q = 1;           // directly loaded records in flight per thread (0: one at a time, in pass 3)
 
 template <bool GOURAUD, int HS = HTS>
 struct ShadeStage {
@@ -925,7 +861,7 @@ struct ShadeStage {
     // a tile stages RT records in KEY_BYTES + EXTRA bytes.
     static constexpr int REC = RecLen<GOURAUD>::REC;
     static constexpr int KEY_BYTES = TH * (TW + 1) * 8;
-    static constexpr int EXTRA = GOURAUD ? NR_REC_EXTRA : 0;
+    static constexpr int EXTRA = GOURAUD ? REC_EXTRA : 0;
     static constexpr int RT_RAW = (KEY_BYTES + EXTRA) / (REC * 8);
     static constexpr int RT = RT_RAW < TH * TW ? RT_RAW : TH * TW;   // staged records per tile
     static constexpr int HT = 0, HIDX = HS * 4, DIDX = HS * 6;
@@ -950,10 +886,7 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
     constexpr int PPT = TH * TW / NT;
     static_assert(PPT <= 32, "overflow bitmask");
     const int tid = opaque_tid();
-#ifndef NR_FLAT_DIRECT
-#define NR_FLAT_DIRECT 1
-#endif
-    if constexpr (!GOURAUD && NR_FLAT_DIRECT) {
+    if constexpr (!GOURAUD) {
         // Flat: a winner's colour is its rgb -- no record to stage, so no
         // winner dedup: each pixel loads its winner's colour itself (the few
         // distinct winners of a tile stay in L2), FQ pixels' loads in flight
@@ -1050,21 +983,14 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
     __syncthreads();   // every key read: the records may overwrite them
     NR_PROBE_STAMP(4);
     const u32 U = nU < (u32)St::RT ? nU : (u32)St::RT;
-#ifndef NR_REC_Q
-#define NR_REC_Q 2
-#endif
-    if constexpr (NR_REC_Q >= 2) {
-        // two winners per thread per round, both records' loads in flight
-        for (u32 u = tid; u < U; u += 2 * NT) {
-            RecordSrc<GOURAUD> s0, s1;
-            const bool two = u + NT < U;
-            load_record_src<GOURAUD>(fp, (i64)didx[u] - 1, s0);
-            if (two) load_record_src<GOURAUD>(fp, (i64)didx[u + NT] - 1, s1);
-            build_record<GOURAUD>(fp, s0, rec + u * St::REC);
-            if (two) build_record<GOURAUD>(fp, s1, rec + (u + NT) * St::REC);
-        }
-    } else {
-        for (u32 u = tid; u < U; u += NT) make_record<GOURAUD>(fp, (i64)didx[u] - 1, rec + u * St::REC);
+    // two winners per thread per round, both records' loads in flight
+    for (u32 u = tid; u < U; u += 2 * NT) {
+        RecordSrc<GOURAUD> s0, s1;
+        const bool two = u + NT < U;
+        load_record_src<GOURAUD>(fp, (i64)didx[u] - 1, s0);
+        if (two) load_record_src<GOURAUD>(fp, (i64)didx[u + NT] - 1, s1);
+        build_record<GOURAUD>(fp, s0, rec + u * St::REC);
+        if (two) build_record<GOURAUD>(fp, s1, rec + (u + NT) * St::REC);
     }
     __syncthreads();
     NR_PROBE_STAMP(5);
@@ -1167,25 +1093,14 @@ __device__ __forceinline__ f64 readlane_f64(f64 v, int lane) {
     return __longlong_as_double((long long)(((u64)hi << 32) | lo));
 }
 
-#ifndef NR_BIG_PX
-#define NR_BIG_PX 32
-#endif
 // A triangle whose bounding box covers at least BIG_PX pixels of the tile is
-// rasterised by the whole wave rather than by its own lane.
-constexpr int BIG_PX = NR_BIG_PX;
+// rasterised by the whole wave rather than by its own lane (96 measured 4-6 %
+// slower on C2).
+constexpr int BIG_PX = 32;
 static_assert(TH <= 64, "coop raster: one lane per tile row");
 constexpr f64 COOP_PAIRS = 2.0;
-
-#ifndef NR_VIS_BASE_PRIO
-#define NR_VIS_BASE_PRIO 0   // wave priority of the other k_vis items (the binning kernels run at 0)
-#endif
-#ifndef NR_HEAVY_PRIO
-#define NR_HEAVY_PRIO 512   // work items of at least this many triangles run at raised wave priority (0: off)
-#endif
-constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
-
-
-
+constexpr u32 HEAVY_PRIO = 512;   // work items of at least this many triangles run at raised wave priority
+constexpr int KS = TW + 1;        // padded row stride of the LDS tile keys
 
 
 // One workgroup per work item (tile, slice of <= SLICE triangles).  The 4
@@ -1200,8 +1115,6 @@ constexpr int KS = TW + 1;     // padded row stride of the LDS tile keys
 // pair density -- the variant without it keeps fewer registers live for sliver meshes.
 // NT: workgroup size (VWG, or 2 * VWG for batches with few pairs, whose dense
 // items are latency-bound: more waves per item).
-// WPE: waves per SIMD the registers are allocated for (NR_VIS_WAVES_PER_EU, or 3 for large batches: see
-// launch_vis).
 // The checks of a warm batch (k_bin_warm): wstat = {pair sum of the set's
 // warm batches since its cursors were zeroed, tag of a batch that found a tile
 // over its range}; the lists are trusted when the sum == expect, the tag word
@@ -1219,8 +1132,8 @@ struct WarmCheck {
     u32* hfail;
 };
 
-template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT, int WPE = NR_VIS_WAVES_PER_EU>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
+template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ kslot, u32* __restrict__ done,
                                              const u32* __restrict__ plan, const WarmCheck wc) {
@@ -1230,9 +1143,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // rows at the same column then hit different LDS banks
     // one LDS block (ShadeStage): hash tables | tile keys | extra; the
     // shading records overwrite the keys
-    // the 3-wave instance has LDS to spare for a larger hash table, and so has
-    // the 512-thread one (two workgroups per CU)
-    constexpr int HS = WPE == 3 ? NR_HTS3 : NT > VWG ? NR_HTS_WIDE : HTS;
+    // the 512-thread instance has LDS to spare for a larger hash table (two
+    // workgroups per CU)
+    constexpr int HS = NT > VWG ? HTS_WIDE : HTS;
     __shared__ __attribute__((aligned(16))) unsigned char lds[ShadeStage<GOURAUD, HS>::BYTES];
     u64* const key = reinterpret_cast<u64*>(lds + ShadeStage<GOURAUD, HS>::KEY_OFF);
     __shared__ u32 zin[ZMODE == 2 ? TH * KS : 1];
@@ -1284,16 +1197,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             le = (u32)((k + 1) * n / nsl);
         }
         constexpr int rlo = 0;
-#if NR_HEAVY_PRIO
-        // the longest work items (dense tiles' slices) set the kernel's
-        // critical path: their waves win the SIMD's issue arbitration over the
-        // short items that run beside them
-#ifndef NR_PRIO_SPLIT
-#define NR_PRIO_SPLIT 1   // the slices of split tiles too (their last slice merges and shades: the longest chains)
-#endif
-        if (le - ls >= (u32)NR_HEAVY_PRIO || (NR_PRIO_SPLIT && multi)) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(NR_VIS_BASE_PRIO);
-#endif
+        // the longest work items (dense tiles' slices, and the slices of split
+        // tiles, whose last slice merges and shades: the longest chains) set
+        // the kernel's critical path: their waves win the SIMD's issue
+        // arbitration over the short items that run beside them
+        if (le - ls >= HEAVY_PRIO || multi) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
         const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
         const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
         const int wlim = (int)(fp.W - x0 < TW ? fp.W - x0 : TW);
@@ -1386,21 +1295,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             edge_slopes(sx, sy, sl);
             const f64 inv = 1.0 / den;
             const u64 id1 = (u64)t + 1;
-#ifndef NR_SPAN32
-#define NR_SPAN32 1
-#endif
             // f32 row spans (row_span32) with the exact f64 row_span_in for the
             // rows the f32 bound cannot decide: C2 -2 %, one rank's 8-way C3
-            // share -3 % (k_vis 44 -> 40 us); the 3-wave instance (C3) keeps the
-            // f64 spans: neutral there at +18 VGPRs (profiles/r03_c3/ab_span32.txt)
-#ifndef NR_SPAN32_WPE3
-#define NR_SPAN32_WPE3 0
-#endif
-#ifndef NR_SPAN32_FLAT
-#define NR_SPAN32_FLAT 0   // flat batches: the f64 spans (the f32 ones cost the flat instances 8-24 B/lane of spills)
-#endif
-            constexpr bool SPAN32 = NR_SPAN32 && (WPE != 3 || NR_SPAN32_WPE3) && (GOURAUD || NR_SPAN32_FLAT) &&
-                                    ZMODE != 2 && !COUNT;
+            // share -3 % (k_vis 44 -> 40 us; profiles/r03_c3/ab_span32.txt).
+            // Flat batches keep the f64 spans (the f32 ones cost the flat
+            // instances 8-24 B/lane of spills).
+            constexpr bool SPAN32 = GOURAUD && ZMODE != 2 && !COUNT;
             // the wave's large triangles first, one at a time, all lanes on each
             // (the keys are an order-free min / max, so the order of the two
             // passes is free; this one reads every lane's screen vertices, so
@@ -1578,39 +1478,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 }
 
 // k_vis runs 2 * VWG-thread workgroups when the last batch had a few dense
-// tiles (>= HEAVY_PAIRS pairs), fewer than NR_WIDE_HEAVY (512, half the chip's
-// k_vis workgroup slots): each dense item is then latency-bound at low
-// occupancy and gains from more waves (C3 sharded 8 ways -18 %, 4 ways
-// -14 %; 2 ways +6 %, hence the threshold); with many dense tiles (C3
-// unsharded, 2 ways) or none (C2) the narrow
-// workgroups are faster.
-static u32 wide_heavy() {
-    static const u32 v = [] {
-        const char* e = getenv("NR_WIDE_HEAVY");
-        return e ? (u32)atol(e) : 512u;
-    }();
-    return v;
-}
-
-// Registers of k_vis for 3 waves per SIMD (up to 168 VGPRs, no spills) on large
-// batches: with one workgroup slot per CU left free by the raster, the next
-// batch's binning kernels run beside it instead of waiting for its tail, and
-// the frame shortens while k_vis itself takes the same time (C3 0.1667 ->
-// 0.1609 ms per frame; profiles/r02_c3/ab_wpe3.txt).  Short batches (C2, an
-// 8-way share) keep 4 waves: their rasters are short and occupancy-bound
-// (+15 % at 3).  NR_VIS_WPE3=0 keeps 4 waves everywhere (A/B).
-// Round 4: off by default.  With the per-item addresses no longer hoisted
-// (opaque_tid) the 4-wave instances need no more than 128 VGPRs without
-// spills, and a warm batch bins inline before its raster, so no binning kernel
-// needs the slot the 3-wave instance left free: C3 0.147 -> 0.140 ms per frame
-// at 4 waves (profiles/r04/ab_instances.txt).  NR_VIS_WPE3=1 forces it (A/B).
-static bool vis_wpe3(bool big) {
-    static const int v = [] {
-        const char* e = getenv("NR_VIS_WPE3");
-        return e ? atoi(e) : 0;
-    }();
-    return v == 2 ? big : v != 0;
-}
+// tiles (>= HEAVY_PAIRS pairs), fewer than WIDE_HEAVY (half the chip's k_vis
+// workgroup slots): each dense item is then latency-bound at low occupancy
+// and gains from more waves (C3 sharded 8 ways -18 %, 4 ways -14 %; 2 ways
+// +6 %, hence the threshold); with many dense tiles (C3 unsharded, 2 ways)
+// or none (C2) the narrow workgroups are faster.  (A 3-wave-per-SIMD
+// instance, which left the next batch's binning a slot beside the raster, was
+// dropped in round 5: 4 waves measured faster once k_vis was spill-free, C3
+// 0.147 -> 0.140 ms, profiles/r04/ab_instances.txt.)
+constexpr u32 WIDE_HEAVY = 512;
 
 // The k_vis inputs of one batch: its work items, pair list and plan totals
 // (a binning set's, or the warm schedule's).
@@ -1623,7 +1499,7 @@ struct VisArgs {
 
 template <int Z, bool C, bool G>
 void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
-                hipEvent_t stop, bool big) {
+                hipEvent_t stop) {
     const WarmCheck wc = va.wc;
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
@@ -1631,16 +1507,13 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
                                   : (sc.lastN == 0 || sc.lastPairs > (u64)(COOP_PAIRS * (f64)sc.lastN));
     // wide workgroups when the last batch had few pairs (a sharded frame):
     // its dense items run at low occupancy and are latency-bound
-    const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wide_heavy();
+    const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < WIDE_HEAVY;
 #define NR_VIS(CO, NTT, ...)                                                                                       \
     hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, nullptr, stop, 0, fp, va.items,  \
                           va.list, sc.kslot, sc.fdone, va.plan, wc)
     if (wide) {
         if (coop) NR_VIS(1, 2 * VWG, false, G, true, 2 * VWG);
         else NR_VIS(0, 2 * VWG, false, G, false, 2 * VWG);
-    } else if (!C && vis_wpe3(big)) {
-        if (coop) NR_VIS(1, VWG, false, G, true, VWG, 3);
-        else NR_VIS(0, VWG, false, G, false, VWG, 3);
     } else if (coop) {
         NR_VIS(1, VWG, C, G, true, VWG);
     } else {
@@ -1651,29 +1524,21 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
 
 template <int Z, bool G>
 void launch_vis_z(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
-                  hipEvent_t stop, bool big) {
-    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, va, grid, s, stop, big);
-    else launch_vis<Z, false, G>(fp, sc, va, grid, s, stop, big);
+                  hipEvent_t stop) {
+    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, va, grid, s, stop);
+    else launch_vis<Z, false, G>(fp, sc, va, grid, s, stop);
 }
 
 static void launch_vis_any(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
-                           hipEvent_t stop, bool big, int zmode, bool g) {
-    if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, va, grid, s, stop, big); else launch_vis_z<1, false>(fp, sc, va, grid, s, stop, big); }
-    else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, va, grid, s, stop, big); else launch_vis_z<2, false>(fp, sc, va, grid, s, stop, big); }
-    else { if (g) launch_vis_z<0, true>(fp, sc, va, grid, s, stop, big); else launch_vis_z<0, false>(fp, sc, va, grid, s, stop, big); }
+                           hipEvent_t stop, int zmode, bool g) {
+    if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, va, grid, s, stop); else launch_vis_z<1, false>(fp, sc, va, grid, s, stop); }
+    else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, va, grid, s, stop); else launch_vis_z<2, false>(fp, sc, va, grid, s, stop); }
+    else { if (g) launch_vis_z<0, true>(fp, sc, va, grid, s, stop); else launch_vis_z<0, false>(fp, sc, va, grid, s, stop); }
 }
 
 // Events of a batch carried by the kernels' own completion signals
 // (hipExtLaunchKernel stop events) instead of separate marker packets: every
-// packet between two rasters on the main queue costs a few microseconds
-// (NR_EXT_STOP=0: hipEventRecord after the launch, for A/B).
-static bool ext_stop() {
-    static const bool v = [] {
-        const char* e = getenv("NR_EXT_STOP");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
+// packet between two rasters on the main queue costs a few microseconds.
 
 // Everything a batch needs to be re-run after an overflow (nr_settle).
 struct PendingBatch {
@@ -1705,54 +1570,14 @@ static void record_known(TriangleBuffer* tb, const BinKey& key, u32 pairs, u32 h
     tb->knownSplit = split;
 }
 
-// Items the plan kernel aims for when it picks the slice length
-// (NR_SLICE_TARGET; the environment variable of the same name overrides it).
-// Round 4 (warm binning, spill-free k_vis): 256, i.e. slices of 1024 for every
-// batch of >= 2^17 owned pairs.  An 8-way C3 share (~150k pairs) used to get
-// slices of 512: its split tiles' slot merges cost more than the longer
-// slices (0.046 -> 0.041 ms per frame, C2 -1 %, C3 unchanged;
-// profiles/r04/ab_slice_target.txt).
-static u32 slice_target() {
-    static const u32 v = [] {
-        const char* e = getenv("NR_SLICE_TARGET");
-        const long x = e ? atol(e) : 0;
-        return x > 0 ? (u32)x : (u32)NR_SLICE_TARGET;
-    }();
-    return v;
-}
+// Split limits of dense tiles (split_limits): a tile of more pairs than
+// min(slice, SPLIT_AT) is split into slices of about DSLICE pairs (SetSplitLimits
+// overrides them per context).
+constexpr u32 SPLIT_AT = 1024, DSLICE = 1024;
 
-// Split limits of dense tiles (split_limits): NR_SPLIT_AT (a tile of more
-// pairs than min(slice, this) is split) and NR_DSLICE (its slices' length).
-#ifndef NR_SPLIT_AT
-#define NR_SPLIT_AT 1024
-#endif
-#ifndef NR_DSLICE
-#define NR_DSLICE 1024
-#endif
-static u32 env_u32(const char* name, u32 dflt) {
-    const char* e = getenv(name);
-    const long x = e ? atol(e) : 0;
-    return x > 0 ? (u32)x : dflt;
-}
-static u32 split_at() {
-    static const u32 v = env_u32("NR_SPLIT_AT", NR_SPLIT_AT);
-    return v;
-}
-static u32 dslice() {
-    static const u32 v = env_u32("NR_DSLICE", NR_DSLICE);
-    return v;
-}
-
-// Binning output sets in rotation (NR_BIN_SETS, 2 or 3): with k sets the
-// binning of batch b waits only for the raster of batch b - k.
-static int bin_sets() {
-    static const int v = [] {
-        const char* e = getenv("NR_BIN_SETS");
-        const int x = e ? atoi(e) : 0;
-        return x == 2 || x == 3 ? x : 3;
-    }();
-    return v;
-}
+// Binning output sets in rotation: with k sets the binning of batch b waits
+// only for the raster of batch b - k.
+constexpr int BIN_SETS = 3;
 
 static hipEvent_t sync_event() {
     hipEvent_t e;
@@ -1907,8 +1732,8 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         // (an ordered batch uses no key slots, and its lists must fit the raster's LDS sort)
         const u32 kcap32 = ordered ? 0xFFFFFFFFu : (u32)std::min<size_t>(sc.kslot_cap / (TH * TW), 0xFFFFFFF0ull);
         const u32 maxc = ordered ? ORD_SORT_CAP : 0u;
-        const u32 sat = sc.splitAt ? sc.splitAt : split_at(), dsl = sc.dslice ? sc.dslice : dslice();
-        if ((plan_reg() && !besideRaster && ntiles <= PLAN_T * PR_MAX) || ordered) {   // (ordered: ntiles <= ORD_BIN_TILES)
+        const u32 sat = sc.splitAt ? sc.splitAt : SPLIT_AT, dsl = sc.dslice ? sc.dslice : DSLICE;
+        if ((!besideRaster && ntiles <= PLAN_T * PR_MAX) || ordered) {   // (ordered: ntiles <= ORD_BIN_TILES)
             // the register plan: one 1024-thread workgroup, PR = tiles per
             // thread -> 4, 8 or 16 (PR 4: 107 VGPRs; PR 8 and 16 spill a few,
             // 4 and 39, at __launch_bounds__(1024)'s 128).  It needs a whole CU
@@ -1922,18 +1747,18 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
             const int per = (ntiles + PLAN_T - 1) / PLAN_T;
 #define NR_PLAN_R(PP) hipLaunchKernelGGL((k_free_plan_r<PLAN_T, PP>), dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, \
                                          fp.tiles_x, fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, \
-                                         (u32)cap, icap32, seq, slice_target(), kcap32, sat, dsl, maxc)
+                                         (u32)cap, icap32, seq, SLICE_TARGET, kcap32, sat, dsl, maxc)
             if (per <= 4) NR_PLAN_R(4); else if (per <= 8) NR_PLAN_R(8); else NR_PLAN_R(16);
 #undef NR_PLAN_R
         }
         else if (besideRaster)
             hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
-                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target(), kcap32, sat, dsl);
+                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, SLICE_TARGET, kcap32, sat, dsl);
         else
             hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
-                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, slice_target(), kcap32, sat, dsl);
+                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, SLICE_TARGET, kcap32, sat, dsl);
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_SCAN, e0, e1, sb);
 
@@ -1943,16 +1768,12 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
             // totals, else the last validated batch's items + 25 % (>= 1024,
             // the chip's k_vis workgroup slots) -- not the capacity bound, whose
             // surplus workgroups (45 % of a C3 launch, 90 % of an 8-way share's)
-            // were dispatched only to exit (NR_GRID_EST=0: the capacity bound)
-            static const bool gridEst = [] {
-                const char* e = getenv("NR_GRID_EST");
-                return e ? atoi(e) != 0 : true;
-            }();
+            // were dispatched only to exit
             // (two or three items per workgroup in turn: C3 k_vis 138 -> 150 / 157 us,
             // profiles/r03_c3/ab_grid_div.txt)
             u64 g = F.fitems_cap;
-            if (gridEst && knownItems) g = knownItems;
-            else if (gridEst && sc.lastItems) g = std::max<u64>((u64)sc.lastItems + sc.lastItems / 4, 1024);
+            if (knownItems) g = knownItems;
+            else if (sc.lastItems) g = std::max<u64>((u64)sc.lastItems + sc.lastItems / 4, 1024);
             grid = (u32)std::min<u64>(std::min<u64>(g, F.fitems_cap), 8192);
             break;
         }
@@ -1976,7 +1797,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     }
 
     nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
-    const bool xs = ext_stop() && sb != sa && !e1;   // no timing events around the kernel
+    const bool xs = sb != sa && !e1;   // no timing events around the kernel
     hipEvent_t binStop = xs ? F.evBin : nullptr;
     hipEvent_t emitStop = ordered ? nullptr : binStop;   // (ordered: the list sort ends the binning)
     if (ldsh) hipExtLaunchKernelGGL(k_free_emit<true>, dim3(gb), dim3(256), (u32)hbytes, sb, nullptr, emitStop, 0, bp, F.foff, F.fcur, F.flist, ntiles, F.frect, (const u32*)F.dplan);
@@ -1998,17 +1819,16 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     bool visDone = false;
     if (ordered) {   // one workgroup per tile, its list sorted in LDS
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-        const bool vs = ext_stop() && !e1;
+        const bool vs = !e1;
         launch_ordered_binned(fp, F.flist, F.foff, F.dplan, F.frec, ntiles, sa, vs ? F.evVis : nullptr);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
     } else if (grid > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-        const bool vs = ext_stop() && !e1;
+        const bool vs = !e1;
         hipEvent_t st = vs ? F.evVis : nullptr;
-        const bool largeShare = owned_share_large(fp.period, fp.mask, src.n);   // owned share >= 2^17 triangles
-        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, 0u, 0u, nullptr}}, grid, sa, st, largeShare, zmode, g);
+        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, 0u, 0u, nullptr}}, grid, sa, st, zmode, g);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
@@ -2019,27 +1839,16 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
 }
 
 // ---- warm binning ---------------------------------------------------------
-// NR_WARM: 0 off, 1 on (default).  NR_WARM_INLINE: 1 bin a warm batch on the
-// main stream right before its raster (no cross-queue wait), 0 on the
-// binning stream beside the previous raster, 2 (default) inline for batches of
-// at least 2^16 triangles: measured (round 4, MI355X) C3 0.1487 -> 0.1445,
-// 1M triangles at 1080p and one rank's 8-way C3 share faster inline; the
-// one-kernel binning beside a running raster slows the raster more than the
-// serial binning costs.
-static bool warm_on(const TriScratch& sc) {
-    static const int v = [] {
-        const char* e = getenv("NR_WARM");
-        return e ? atoi(e) : 1;
-    }();
-    return sc.warmMode ? sc.warmMode == 1 : v != 0;
-}
+// On unless SetWarmBinning(2).
+static bool warm_on(const TriScratch& sc) { return sc.warmMode != 2; }
 // Warm binning inline (main stream, right before the raster) or beside the
 // previous raster (binning stream).  Inline when the rank's owned share of
 // the batch is large: 1M triangles unsharded 0.154 -> 0.140 ms per frame,
 // neutral at 2 shards; beside the raster for small batches (C2 0.065 ->
 // 0.058 ms) and for the smaller shares, whose active binning blocks fit
 // beside the raster (8-way 0.0505 -> 0.046-0.048 ms, 4-way -1 %;
-// profiles/r04/ab_warm_blocks.txt).
+// profiles/r04/ab_warm_blocks.txt).  NR_WARM_INLINE: 1 always inline, 0
+// always beside (A/B).
 static bool warm_inline(i64 n, int period, u64 mask) {
     static const int v = [] {
         const char* e = getenv("NR_WARM_INLINE");
@@ -2148,13 +1957,6 @@ __global__ void k_gate_wait(const u32* __restrict__ gate, u32 tok, const u32* __
     }
     for (int k = 0; k < 4; ++k) gplan[k] = (k == 3 && !ok) ? 0u : splan[k];   // {pairs, items, slices, fits}
 }
-static bool gate_on() {   // NR_GATE=0: the cross-queue event wait (A/B)
-    static const bool v = [] {
-        const char* e = getenv("NR_GATE");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
 
 // The binning blocks (256 * TPT triangles) of a schedule with a cluster that
 // may reach an owned tile: cluster_may_touch on the host over the buffer's
@@ -2230,7 +2032,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     hipStream_t sb = warm_inline(bp.src.n, fp.period, fp.mask) ? sa : nr_bin_stream_for(ctx->device);
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const int si = sc.fnext;
-    sc.fnext = (sc.fnext + 1) % bin_sets();
+    sc.fnext = (sc.fnext + 1) % BIN_SETS;
     TriScratch::FreeSet& F = sc.fset[si];
     if (!F.evBin) { F.evBin = sync_event(); F.evVis = sync_event(); }
     if (!sc.hfail) {
@@ -2281,14 +2083,14 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const int gb = (int)((bp.src.n + 256 * TPT - 1) / (256 * TPT));
     hipEvent_t e0, e1;
     nr_timing_begin_on(ctx, NRK_TRI_EMIT, &e0, &e1, sb);
-    const bool gated = sb != sa && gate_on() && !e1;   // same-queue hand-off (k_gate_wait) instead of an event wait
+    const bool gated = sb != sa && !e1;   // same-queue hand-off (k_gate_wait) instead of an event wait
     if (gated && !F.gate) {
         NR_CHECK(hipMalloc(&F.gate, 4 * sizeof(u32)));
         NR_CHECK(hipMalloc(&F.gplan, 4 * sizeof(u32)));
         NR_CHECK(hipMemset(F.gate, 0, 4 * sizeof(u32)));
         F.gateTok = 0;
     }
-    const bool xs = ext_stop() && sb != sa && !e1 && !gated;
+    const bool xs = sb != sa && !e1 && !gated;
     hipEvent_t binStop = xs ? F.evBin : nullptr;
     const u32 epoch = F.curEpoch++;
     if (++sc.warmTag == 0) sc.warmTag = 1;
@@ -2296,17 +2098,9 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     u32* const wstat = F.fcur + ntiles;   // {pair sum, error tag} (WS_SUM, WS_TAG)
     const int inject = sc.warmInject;
     sc.warmInject = 0;
-    // cluster culling of the rank's tile rows (NR_CLUSTER_CULL=0: off, A/B)
-    static const bool cullOn = [] {
-        const char* e = getenv("NR_CLUSTER_CULL");
-        return e ? atoi(e) != 0 : true;
-    }();
-    const f64* cbox = cullOn && S.anyCull ? tbCbox : nullptr;
-    static const bool blocksOn = [] {   // NR_WARM_BLOCKS=0: launch every block (A/B)
-        const char* e = getenv("NR_WARM_BLOCKS");
-        return e ? atoi(e) != 0 : true;
-    }();
-    const bool useBlocks = blocksOn && cbox && S.blocksGen == S.gen;
+    // cluster culling of the rank's tile rows, and only the schedule's active blocks launched
+    const f64* cbox = S.anyCull ? tbCbox : nullptr;
+    const bool useBlocks = cbox && S.blocksGen == S.gen;
     const u32* blocks = useBlocks ? S.blocks : nullptr;
     const int grid = useBlocks ? (int)S.nblocks : gb;
     if (grid > 0) {
@@ -2341,11 +2135,10 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     bool visDone = false;
     if (S.nitems > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-        const bool vs = ext_stop() && !e1;
+        const bool vs = !e1;
         const WarmCheck wc{wstat, tag, (epoch + 1) * S.pairs, sc.dfail};
         launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa,
-                       vs ? F.evVis : nullptr, owned_share_large(fp.period, fp.mask, bp.src.n), zmode,
-                       fp.src.gouraud != 0);
+                       vs ? F.evVis : nullptr, zmode, fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
@@ -2371,12 +2164,6 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     bp.W = ctx->width; bp.H = ctx->height; bp.tiles_x = fp.tiles_x;
     bp.period = fp.period; bp.mask = fp.mask;
     set_owned_rows(bp, fp.tiles_y);
-    if (!ordered && gvis_wanted(ctx, src, ctx->tri.srcMeanArea)) {   // small triangles: no binning
-        draw_gvis(ctx, src, fp, bp);
-        ctx->lastPath = 3;
-        finish_batch(ctx, fp);
-        return;
-    }
     // fragment counting reads a counter back anyway: run exact (synchronous);
     // so does a batch from the caller's device arrays: a deferred overflow
     // re-run (settle, at the next call) could read them after the caller has
@@ -2393,13 +2180,8 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     // 0.1640 -> 0.1614 ms, C2 0.0685 -> 0.062 ms with known sizes; an emulated
     // rank share of 4 / 8 shards 0.066 -> 0.076 / 0.054 -> 0.062 ms, where the
     // host wait on the plan paces the binning; profiles/r02_c3/ab_known.txt).
-    // NR_KNOWN_SIZES=0 / 2: never / also for sharded batches (A/B).
-    static const int knownMode = [] {
-        const char* e = getenv("NR_KNOWN_SIZES");
-        return e ? atoi(e) : 1;
-    }();
     // (ordered batches are always validated: their plan also checks the list lengths)
-    const bool known = !ordered && knownMode != 0 && (fp.period == 1 || knownMode == 2) && tb && tb->known &&
+    const bool known = !ordered && fp.period == 1 && tb && tb->known &&
                        !sc.capOverride && memcmp(&tb->knownKey, &key, sizeof key) == 0;
     if (known && !exact) {   // this batch's totals pick the k_vis variant (launch_vis)
         sc.lastN = (u64)src.n;
@@ -2419,7 +2201,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         return;
     }
     const int si = sc.fnext;
-    sc.fnext = (sc.fnext + 1) % bin_sets();
+    sc.fnext = (sc.fnext + 1) % BIN_SETS;
     u32 seq = 0;
     static const bool pipeOn = [] {   // NR_BIN_PIPE=0: bin on the main stream (A/B, isolated kernel times)
         const char* e = getenv("NR_BIN_PIPE");
@@ -2429,13 +2211,9 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
     // or a Flush) has no raster to overlap its binning with: it bins in line
     // on the main stream, with the wide plan kernel, and k_vis follows without
     // a cross-queue wait (whose wake-up took ~15 us in the kernel trace,
-    // profiles/r02h_c3).  NR_BIN_IDLE_INLINE=0: always the binning stream (A/B).
-    static const bool idleInline = [] {
-        const char* e = getenv("NR_BIN_IDLE_INLINE");
-        return e ? atoi(e) != 0 : true;
-    }();
+    // profiles/r02h_c3).
     bool idle = false;
-    if (idleInline && pipeOn && tb != nullptr && !exact) {
+    if (pipeOn && tb != nullptr && !exact) {
         const hipError_t q = hipStreamQuery(ctx->stream);
         idle = q == hipSuccess;
         if (q == hipErrorNotReady) (void)hipGetLastError();   // an answer, not a failure

@@ -559,13 +559,8 @@ void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* of
 }
 
 void draw_ordered(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned) {
-    // NR_ORD_BINNED=0: always the global-sort path (A/B)
-    static const bool binned = [] {
-        const char* e = getenv("NR_ORD_BINNED");
-        return e ? atoi(e) != 0 : true;
-    }();
     const i64 ntiles = (i64)((ctx->width + TW - 1) / TW) * ((ctx->height + TH - 1) / TH);
-    if (binned && ntiles <= ORD_BIN_TILES) {
+    if (ntiles <= ORD_BIN_TILES) {
         draw_free(ctx, src, tb, callerOwned, true);
         return;
     }

@@ -1,10 +1,8 @@
-// nr_tri_shade.h — per-pixel pieces shared by the order-free rasterisers
-// (nr_tri_free.hip: tiled k_vis; nr_tri_gvis.hip: whole-frame visibility
-// buffer): the depth of one fragment as a packed visibility key, and the
+// nr_tri_shade.h — per-pixel pieces of the order-free raster (nr_tri_free.hip,
+// k_vis): the depth of one fragment as a packed visibility key, and the
 // deferred shading of a pixel from its winning triangle (record ->
 // barycentrics -> colour -> ApplyPixel, cpp:515-549 -> framebuffer, depth and
-// frame output).  Both rasterisers must produce the same bits, so they share
-// these expressions.
+// frame output).
 #pragma once
 
 #include "nr_tri.h"

@@ -425,12 +425,7 @@ class RenderContext:
             raise RuntimeError("GatherFramebuffer failed: " + _lib.last_error())
 
     def last_raster_path(self) -> str:
-        return {0: "none", 1: "order-free", 2: "ordered", 3: "order-free-frame"}[lib.GetLastRasterPath(self._ptr)]
-
-    def set_frame_vis_raster(self, mode: int):
-        """Opaque Z LESS + write batches: 0 automatic (the whole-frame
-        visibility buffer for small triangles), 1 always, 2 never (tiled)."""
-        lib.SetFrameVisRaster(self._ptr, int(mode))
+        return {0: "none", 1: "order-free", 2: "ordered"}[lib.GetLastRasterPath(self._ptr)]
 
     def set_warm_binning(self, mode: int):
         """A TriangleBuffer drawn again under the binning key of its last

@@ -31,22 +31,6 @@ def gpu():
 
 
 @pytest.fixture(scope="session")
-def gpu_frame(gpu):
-    """The HIP library with every opaque Z LESS + write batch on the whole-frame
-    visibility buffer (SetFrameVisRaster(1)), whatever its triangle sizes."""
-    import scenes
-    return scenes.GpuFactory(frame_vis=1)
-
-
-@pytest.fixture(scope="session")
-def gpu_tiled(gpu):
-    """The HIP library with the whole-frame visibility buffer off (SetFrameVisRaster(2)):
-    every opaque batch takes the tiled k_vis path."""
-    import scenes
-    return scenes.GpuFactory(frame_vis=2)
-
-
-@pytest.fixture(scope="session")
 def golden():
     import numpy as np
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "scenes.npz")))

@@ -190,16 +190,12 @@ class OracleFactory:
 class GpuFactory:
     name = "gpu"
 
-    def __init__(self, frame_vis=0):
+    def __init__(self):
         from libnativecpurenderer_amd import libNativeCPURendererPybind as R
         self.R = R
-        self.frame_vis = frame_vis   # SetFrameVisRaster of every context (0: automatic)
 
     def context(self, w, h, alpha):
-        ctx = self.R.RenderContext(w, h, alpha)
-        if self.frame_vis:
-            ctx.set_frame_vis_raster(self.frame_vis)
-        return ctx
+        return self.R.RenderContext(w, h, alpha)
 
     def texture(self, arr):
         return self.R.Texture.from_numpy(arr)

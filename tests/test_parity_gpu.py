@@ -89,56 +89,13 @@ def test_vis_variants_match_oracle(gpu, oracle, mode):
             assert_same(outs[0], outs[1], f"mode={mode} depth={depth} write={write} alpha={alpha}")
 
 
-def test_c3_gouraud_depth_4k(gpu, gpu_frame, gpu_tiled, oracle):
-    """C3 at full size on both order-free rasterisers (the tiled k_vis the
-    automatic choice takes, and the whole-frame visibility buffer) against one
-    oracle frame."""
+def test_c3_gouraud_depth_4k(gpu, oracle):
+    """C3 at full size (the tiled k_vis) against the oracle frame."""
     xy, z, c = scenes.sphere_mesh(3840, 2160, 500, 1000)
     o, _ = _tri_frame(oracle, 3840, 2160, xy, z, c)
-    for fac, path in ((gpu, "order-free"), (gpu_frame, "order-free-frame"), (gpu_tiled, "order-free")):
-        g, ctx = _tri_frame(fac, 3840, 2160, xy, z, c)
-        assert ctx.last_raster_path() == path
-        assert_same(g, o, "C3 " + path)
-
-
-def _gvis_state_frames(fac, W, H, parts):
-    """Frames that walk the whole-frame visibility buffer's key state: repeated
-    frames from the same pending depth clear (keys reused), a second batch in
-    the same frame (keys from the depth buffer), a clear to another depth, a
-    tiled batch in between, and a resize."""
-    a, b, c = parts
-    ctx = fac.context(W, H, False)
-    outs = []
-    for f in range(3):
-        ctx.set_color(0.2, 0.2, 0.2, 0.2)
-        ctx.set_depth_state(True, True)
-        ctx.clear_depth()
-        ctx.draw_triangles(a[0], a[2], z=a[1])
-        if f == 1:
-            ctx.draw_triangles(b[0], b[2], z=b[1])              # no pending clear: keys from the depth buffer
-        if f == 2:
-            ctx.set_depth_state(True, False)
-            ctx.draw_triangles(c[0], c[2], z=c[1])              # Z test without write (k_vis)
-            ctx.set_depth_state(True, True)
-            ctx.clear_depth(0x90000000)
-            ctx.draw_triangles(b[0], b[2], z=b[1])              # another clear value
-        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
-    ctx.resize(W - 7, H + 5)
-    ctx.set_color(0.3, 0.3, 0.3, 0.3)
-    ctx.clear_depth()
-    ctx.draw_triangles(a[0], a[2], z=a[1])
-    outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
-    return outs
-
-
-def test_frame_vis_key_state(gpu_frame, oracle):
-    W, H = 211, 149
-    parts = [scenes.triangle_soup(2500, W, H, s, seed=90 + k, gouraud=True, zrange=(-0.1, 1.1))
-             for k, s in enumerate((5.0, 12.0, 30.0))]
-    g = _gvis_state_frames(gpu_frame, W, H, parts)
-    o = _gvis_state_frames(oracle, W, H, parts)
-    for k, (x, y) in enumerate(zip(g, o)):
-        assert_same(x, y, f"frame {k}")
+    g, ctx = _tri_frame(gpu, 3840, 2160, xy, z, c)
+    assert ctx.last_raster_path() == "order-free"
+    assert_same(g, o, "C3 order-free")
 
 
 def test_c5_blend_overdraw_reduced(gpu, oracle):
@@ -494,8 +451,8 @@ def _set_shard(ctx, n, r, slots):
 
 @pytest.mark.parametrize("nshards,slots", [(2, None), (3, None), (8, None), (2, [3, 1]), (3, [1, 4, 2]),
                                            (8, [5, 2, 2, 2, 2, 2, 2, 2])])
-@pytest.mark.parametrize("opaque,frame_vis", [(True, 2), (True, 1), (False, 0)])
-def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque, frame_vis):
+@pytest.mark.parametrize("opaque", [True, False])
+def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque):
     """Every shard renders only its tile rows (equal shards, or weighted
     SetShardSlots patterns); the owned rows of all shards put together are
     byte-identical to the unsharded frame (colour + depth), for both
@@ -507,8 +464,6 @@ def test_sharded_frames_assemble_to_the_full_frame(gpu, nshards, slots, opaque, 
 
     def render(n, r):
         ctx = gpu.context(W, H, False)
-        if frame_vis:   # opaque: the tiled k_vis (2) or the whole-frame visibility buffer (1)
-            ctx.set_frame_vis_raster(frame_vis)
         _set_shard(ctx, n, r, slots if n > 1 else None)
         if n > 1:
             from libnativecpurenderer_amd import sharding

@@ -100,7 +100,7 @@ def test_warm_fault_falls_back_exactly(gpu, oracle, mode, mesh_rc):
     W, H = 640, 400
     scene = _scene(W, H, mesh_rc)
     want, _ = _frames(oracle, W, H, scene, 7)
-    _lib.clear_last_error()
+    _lib.clear_error()
     got, ctx = _frames(gpu, W, H, scene, 7, inject=(3, mode))
     for k, (g, o) in enumerate(zip(got, want)):
         assert scenes.bits_equal(g["f64"], o["f64"]), f"frame {k}: {scenes.first_mismatch(g['f64'], o['f64'])}"

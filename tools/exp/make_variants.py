@@ -3,7 +3,7 @@ tools/exp/<name>.so (A/B timing only; never shipped).  Named variants:
   e1 no shading of single-slice tiles   e2 + no pixel loop   e3 + no row loop   e4 + no raster
   times  per-work-item start/end clocks (ExpGetItemTimes, tools/exp/item_times.py)
 Other variants: name=DEF=VAL+DEF2=VAL (compile-time knobs, e.g. NR_VWG, NR_SLICE).
-Usage: python tools/exp/make_variants.py [names...]; load one with NR_LIB=tools/exp/<name>.so (bench.py, tests)."""
+Usage: python tools/exp/make_variants.py [names...]; load one with bench.py --lib tools/exp/<name>.so."""
 import os
 import subprocess
 import sys

@@ -14,8 +14,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import bench  # noqa: E402
-from libnativecpurenderer_amd import libNativeCPURendererPybind as R  # noqa: E402
 from libnativecpurenderer_amd import _lib  # noqa: E402
+if os.environ.get("NR_LIB"):   # (tools only: the probe build instead of the shipped library)
+    _lib.LIB_PATH = os.path.abspath(os.environ["NR_LIB"])
+from libnativecpurenderer_amd import libNativeCPURendererPybind as R  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c3"
 shards = int(sys.argv[2]) if len(sys.argv) > 2 else 1
