@@ -202,6 +202,19 @@ void EndCommandList(RenderContext* ctx);         /* run the queue, stop queueing
 void FlushCommandList(RenderContext* ctx);       /* run the queue, keep queueing (end of a frame) */
 i64 GetCommandListLength(RenderContext* ctx);    /* draws queued and not yet run */
 bool IsRecordingCommands(RenderContext* ctx);
+/* A frame's draw and state calls as ONE packed f64 array (replaces the reference's
+ * per-call ctypes round trips, Pybind:74-300; its unfinished frame recorder is
+ * Pybind:302-367).  Command = opcode word + fixed arguments, run in order through
+ * the same entry points as the single calls (bit-identical):
+ *   0 SaveContextState  1 RestoreContextState  2 SetTransform a..f  3 ApplyTransform a..f
+ *   4 Scale sx sy  5 Translate tx ty  6 Rotate angle  7 SetColorTransform rgba
+ *   8 ApplyColorTransform rgba  9 SetColor rgba  10 FillColor rgba
+ *   11 DrawTexture tex x y w h  12 DrawSplittedTexture tex x y w h uS uE vS vE
+ *   13 DrawRect x y w h rgba  14 DrawLine x1 y1 x2 y2 width rgba  15 DrawCircle x y radius rgba
+ *   16 DrawVerticalGrd x y w h top-rgba bottom-rgba  17 SetPixel x y rgba  18 ApplyPixel x y rgba
+ * (tex: index into `textures`).  Returns the commands run, -1 on a malformed array
+ * (the commands before the bad one have run; error latched). */
+i64 ExecuteCommands(RenderContext* ctx, const f64* words, i64 nwords, Texture* const* textures, i64 ntextures);
 
 /* ---- NEW: device, sync, interop, errors, measurement --------------------- */
 bool SetDevice(i64 device);                      /* device for objects created next on this thread */

@@ -436,6 +436,11 @@ class RenderContext:
     def warm_batch_count(self) -> int:
         return lib.GetWarmBatchCount(self._ptr)
 
+    def packed(self) -> "PackedCommands":
+        """A packing front end of this context: its draw and state calls go
+        to the library as one array per submit() (ExecuteCommands)."""
+        return PackedCommands(self)
+
     def set_warm_fault_injection(self, mode: int):
         """Testing: a fault in the next warm batch (1 tile ranges overflow, 2
         the binning's token is withheld, 3 a workgroup's pairs are dropped);
@@ -515,6 +520,122 @@ class HostBuffer:
         if getattr(self, "ptr", None):
             lib.FreeHostBuffer(self.ptr)
             self.ptr = None
+
+
+class PackedCommands:
+    """A RenderContext's draw and state calls packed on the host and submitted
+    as ONE array per frame (ExecuteCommands) instead of one ctypes round trip
+    per call -- the batching the reference's frame recorder
+    MultiThreadedVideoRenderContextPreparer (Pybind:302-367) set out to do.
+
+    It has the RenderContext methods a frame is drawn with (same names,
+    arguments and results: every command runs through the same entry point, in
+    order); anything else (get_transform, readbacks, triangles, ...) first
+    submits what is packed and then goes to the context itself, so the two can
+    be mixed freely.  Typical use: `cmds = ctx.packed()`, draw the frame through
+    `cmds`, `cmds.submit()` (inside begin_commands()/flush_commands() the draws
+    then run as one launch)."""
+
+    __slots__ = ("_ctx", "_q", "_tex", "_tidx")
+
+    def __init__(self, ctx: "RenderContext"):
+        self._ctx = ctx
+        self._q = []        # f64 words
+        self._tex = []      # textures referenced by this submission (kept alive until it runs)
+        self._tidx = {}
+
+    def _t(self, tex) -> int:
+        p = tex._ptr
+        i = self._tidx.get(p)
+        if i is None:
+            i = self._tidx[p] = len(self._tex)
+            self._tex.append(tex)
+        return i
+
+    def submit(self) -> int:
+        """Runs the packed commands; returns how many ran."""
+        if not self._q:
+            return 0
+        import array
+        words = array.array("d", self._q)
+        tex = (ctypes.c_void_p * max(len(self._tex), 1))(*[t._ptr for t in self._tex])
+        n = lib.ExecuteCommands(self._ctx._ptr, words.buffer_info()[0], len(words), tex, len(self._tex))
+        self._q.clear()
+        self._tex.clear()
+        self._tidx.clear()
+        if n < 0:
+            raise RuntimeError("ExecuteCommands failed: " + _lib.last_error())
+        return n
+
+    def __getattr__(self, name):
+        self.submit()
+        return getattr(self._ctx, name)
+
+    # state (opcodes 0-10, ExecuteCommands)
+    def save_state(self):
+        self._q.append(0.0)
+
+    def restore_state(self):
+        self._q.append(1.0)
+
+    def set_transform(self, a, b, c, d, e, f):
+        self._q += (2.0, a, b, c, d, e, f)
+
+    def apply_transform(self, a, b, c, d, e, f):
+        self._q += (3.0, a, b, c, d, e, f)
+
+    def scale(self, sx, sy):
+        self._q += (4.0, sx, sy)
+
+    def translate(self, tx, ty):
+        self._q += (5.0, tx, ty)
+
+    def rotate(self, angle):
+        self._q += (6.0, angle)
+
+    def rotate_degree(self, deg):
+        self._q += (6.0, deg * math.pi / 180)   # (RenderContext.rotate_degree's expression)
+
+    def set_color_transform(self, r, g, b, a):
+        self._q += (7.0, r, g, b, a)
+
+    def apply_color_transform(self, r, g, b, a):
+        self._q += (8.0, r, g, b, a)
+
+    def set_color(self, r, g, b, a):
+        self._q += (9.0, r, g, b, a)
+
+    def fill_color(self, r, g, b, a):
+        self._q += (10.0, r, g, b, a)
+
+    # draws (opcodes 11-18)
+    def draw_texture(self, tex, x, y, w, h):
+        self._q += (11.0, self._t(tex), x, y, w, h)
+
+    def draw_splitted_texture(self, tex, x, y, width, height, u_start, u_end, v_start, v_end):
+        self._q += (12.0, self._t(tex), x, y, width, height, u_start, u_end, v_start, v_end)
+
+    def draw_rect(self, x, y, width, height, r, g, b, a):
+        self._q += (13.0, x, y, width, height, r, g, b, a)
+
+    def draw_line(self, x0, y0, x1, y1, width, r, g, b, a):
+        self._q += (14.0, x0, y0, x1, y1, width, r, g, b, a)
+
+    def draw_circle(self, x, y, radius, r, g, b, a):
+        self._q += (15.0, x, y, radius, r, g, b, a)
+
+    def draw_vertical_grd(self, x, y, width, height, top_r, top_g, top_b, top_a,
+                          bottom_r, bottom_g, bottom_b, bottom_a):
+        self._q += (16.0, x, y, width, height, top_r, top_g, top_b, top_a, bottom_r, bottom_g, bottom_b, bottom_a)
+
+    def draw_vertical_mut_grd(self, x, y, width, height, steps):
+        RenderContext.draw_vertical_mut_grd(self, x, y, width, height, steps)   # (bands -> draw_vertical_grd here)
+
+    def set_pixel(self, x: int, y: int, r, g, b, a):
+        self._q += (17.0, int(x), int(y), r, g, b, a)
+
+    def apply_pixel(self, x: int, y: int, r, g, b, a):
+        self._q += (18.0, int(x), int(y), r, g, b, a)
 
 
 class RecordingRenderContext(RenderContext):

@@ -213,6 +213,24 @@ class GpuRecordingFactory(GpuFactory):
         return ctx
 
 
+class GpuPackedFactory(GpuFactory):
+    """The HIP library through PackedCommands: a scene's draw and state calls
+    are packed on the host and submitted as one ExecuteCommands array before
+    anything else (readbacks, triangles, ...) touches the context; with
+    `recording`, inside a command list too (one launch per submission)."""
+    name = "gpu-packed"
+
+    def __init__(self, recording=False):
+        super().__init__()
+        self.recording = recording
+
+    def context(self, w, h, alpha):
+        ctx = super().context(w, h, alpha)
+        if self.recording:
+            ctx.begin_commands()
+        return ctx.packed()
+
+
 # ---------------------------------------------------------------------------
 # inputs
 # ---------------------------------------------------------------------------

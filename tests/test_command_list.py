@@ -93,3 +93,52 @@ def test_recording_context_frames(gpu, oracle):
         assert ctx.command_list_length() == 0
         assert scenes.bits_equal(ctx.get_buffer_numpy(), ref.get_buffer_numpy()), f
     assert ctx.frames == 3
+
+
+@pytest.mark.parametrize("recording", [False, True])
+@pytest.mark.parametrize("name", sorted(n for n in scenes.all_scenes() if not n.startswith("tri_")))
+def test_packed_scene_parity(oracle, golden, name, recording):
+    """Every primitive scene through PackedCommands (one ExecuteCommands array
+    per run of draw / state calls), immediate and inside a command list."""
+    g = scenes.run_scene(name, scenes.GpuPackedFactory(recording))
+    o = scenes.run_scene(name, oracle)
+    assert_same(g, o, f"packed {name}")
+
+
+@pytest.mark.parametrize("alpha", [False, True])
+@pytest.mark.parametrize("seed", [41, 42])
+def test_packed_mix_large(oracle, alpha, seed):
+    kw = dict(W=333, H=157, alpha=alpha, n=600, seed=seed, flushes=seed == 42)
+    assert_same(scenes.scene_primitive_mix(scenes.GpuPackedFactory(True), **kw),
+                scenes.scene_primitive_mix(oracle, **kw), f"packed mix seed={seed} alpha={alpha}")
+
+
+def test_execute_commands_rejects_malformed_arrays(gpu):
+    """A malformed array runs its commands up to the bad one and reports -1
+    with a latched error: unknown opcode, truncated command, texture index out
+    of range, fractional pixel coordinate."""
+    import ctypes
+    from libnativecpurenderer_amd import _lib
+    lib = _lib.load()
+    tex = gpu.texture(scenes.pattern_u8(8, 8, 4, seed=3))
+    texs = (ctypes.c_void_p * 1)(tex._ptr)
+
+    def run(words):
+        ctx = gpu.context(32, 16, False)
+        ctx.set_color(0, 0, 0, 0)
+        arr = np.asarray(words, dtype=np.float64)
+        _lib.clear_error()
+        n = lib.ExecuteCommands(ctx._ptr, arr.ctypes.data, len(arr), texs, 1)
+        return n, _lib.last_error(), ctx.get_buffer_numpy()
+
+    rect = [13, 0, 0, 8, 8, 1, 0, 0, 1]           # DrawRect: red 8x8
+    n, err, fb = run(rect + [99])
+    assert n == -1 and "unknown opcode" in err and fb[2, 2, 0] == 1.0
+    n, err, fb = run(rect + [13, 0, 0, 4])
+    assert n == -1 and "truncated" in err and fb[2, 2, 0] == 1.0
+    n, err, fb = run(rect + [11, 1, 0, 0, 8, 8])
+    assert n == -1 and "texture index" in err
+    n, err, fb = run(rect + [17, 1.5, 2, 0, 1, 0, 1])
+    assert n == -1 and "pixel coordinate" in err
+    n, err, fb = run(rect + [11, 0, 10, 0, 8, 8] + [5, 1.0, 2.0])   # + a texture and a translate: 3 commands
+    assert n == 3 and err == ""
