@@ -51,6 +51,10 @@ CONFIGS = {
     # name: (W, H, kind, params)
     "c3": dict(W=3840, H=2160, mesh=(500, 1000), gouraud=True, desc="C3: 1M-tri displaced UV sphere, 3840x2160, Gouraud, Z LESS+write"),
     "c3_1080p": dict(W=1920, H=1080, mesh=(500, 1000), gouraud=True, desc="1M-tri displaced UV sphere, 1920x1080, Gouraud, Z LESS+write (the metric's literal configuration)"),
+    "c3_animated": dict(W=3840, H=2160, mesh=(500, 1000), gouraud=True, animate=True,
+                        desc="C3 with the transform changed every frame (a sub-pixel translate alternating between "
+                             "0 and 0.37 px, as milrenderer.py:980-1010 re-transforms every note every frame): every "
+                             "frame bins cold (count -> plan -> emit), no warm schedule"),
     "c2": dict(W=1920, H=1080, soup=(10000, 32.0, None), gouraud=False, desc="C2: 10k random opaque tris, 1920x1080, flat, Z LESS+write"),
     "c5": dict(W=1920, H=1080, soup=(50000, 256.0, (0.2, 0.8)), gouraud=False, write=False,
                desc="C5: 50k alpha-blended tris back-to-front, 1920x1080, Z test on, write off"),
@@ -226,7 +230,13 @@ class Runner:
         ctx.set_color(0, 0, 0, 0)
         ctx.set_depth_state(True, self.cfg.get("write", True))
         ctx.clear_depth()
-        ctx.draw_triangle_buffer(self.buf)
+        if self.cfg.get("animate"):   # a new transform every frame: the binning key changes
+            ctx.save_state()
+            ctx.translate(0.37 * (i % 2), 0.0)
+            ctx.draw_triangle_buffer(self.buf)
+            ctx.restore_state()
+        else:
+            ctx.draw_triangle_buffer(self.buf)
         ctx.gather_frame_u8(self.comm, 0)
         if self.host is not None and self.rank == 0:
             # frame i's D2H runs on the gather stream while frame i+1 renders;
@@ -257,16 +267,19 @@ class Runner:
     def run(self, steps, warmup, calibrate=False):
         import torch
         ctx, dist = self.ctx, self.dist
-        # fragment count of one frame (outside the timed region), summed over ranks
+        # fragment count of one frame (outside the timed region), summed over
+        # ranks; an animated workload: the mean over its two transforms
         ctx.set_fragment_counting(True)
-        self.frame()
+        nf = 2 if self.cfg.get("animate") else 1
+        for i in range(nf):
+            self.frame(i)
         self.drain()
-        frags = ctx.get_fragment_count()
+        frags = ctx.get_fragment_count() / nf
         ctx.set_fragment_counting(False)
         if dist is not None:
-            t = torch.tensor([frags], dtype=torch.int64, device=self.rdev)
+            t = torch.tensor([frags], dtype=torch.float64, device=self.rdev)
             dist.all_reduce(t)
-            frags = int(t.item())
+            frags = float(t.item())
 
         # partition calibration (N>1, --root-slots auto): every candidate share
         # of rank 0 is timed over a few frames (max over ranks), the fastest kept
@@ -322,6 +335,7 @@ class Runner:
         ctx.reset_kernel_timing()
         ctx.set_kernel_timing_filter("" if not timing else dom)
         self.sync()
+        warm0 = ctx.warm_batch_count()
         t0 = time.perf_counter()
         for i in range(steps):
             ctx.enable_kernel_timing(timing and i % EVENT_EVERY == 0)
@@ -332,6 +346,7 @@ class Runner:
         if dist is not None:
             dist.barrier()
         ctx.enable_kernel_timing(False)
+        warm_frames = ctx.warm_batch_count() - warm0
         ms = dt / steps * 1e3
         tot, cnt = ctx.get_kernel_timing(dom)
         dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
@@ -352,12 +367,13 @@ class Runner:
             "value": round(frags * steps / dt / 1e6, 1),
             "ms_per_step": round(ms, 4),
             "fps": round(1e3 / ms, 1),
-            "fragments_per_frame": int(frags),
+            "fragments_per_frame": int(round(frags)),
             "roofline": roof,
             "raster_path": path,
             "kernel_us": kernels,
             "slots": slots,
             "calib": calib,
+            "warm_binned_frames": warm_frames,
         }
         if path == "ordered" and self.cfg.get("soup", (0, 0, None))[2] is not None:
             # C5: the blend loop is bound by f64 VALU issue, not by HBM (per
@@ -439,7 +455,8 @@ def main():
     extra = {}
     do_extra = args.extra if args.extra is not None else (world == 1 and nsh == 1)
     if do_extra and world == 1:
-        jobs = [("c3_1080p", "none", None), ("c2", "none", None), ("c5", "none", None), (args.config, "host", None),
+        jobs = [("c3_1080p", "none", None), ("c3_animated", "none", None), ("c2", "none", None), ("c5", "none", None),
+                (args.config, "host", None),
                 (args.config, "host", "yuv420p"), ("c2", "host", None)]
         for name, dl, fo in jobs:
             if name == args.config and dl == args.deliver and (fo or args.frame_output) == args.frame_output:
@@ -452,7 +469,8 @@ def main():
             extra[key] = {"workload": sub.cfg["desc"] + what,
                           "triangles": sub.n_tri, **{k: r[k] for k in ("value", "ms_per_step", "fps",
                                                                          "fragments_per_frame", "roofline",
-                                                                         "raster_path", "kernel_us")},
+                                                                         "raster_path", "kernel_us",
+                                                                         "warm_binned_frames")},
                           **({"valu_roofline": r["valu_roofline"]} if "valu_roofline" in r else {})}
             if dl == "host":
                 extra[key]["host_frame_bytes"] = int(np.prod(sub.ctx.frame_output_shape()))
