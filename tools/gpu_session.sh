@@ -10,6 +10,7 @@
 #   ctrace[:ARGS]   rocprofv3 --kernel-trace --memory-copy-trace of bench.py ARGS
 #   stats[:ARGS]    rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   ab:ENV1%ENV2%.. bench lines under each environment (ENVk = A=1+B=2), twice, interleaved; BENCH_ARGS env for the bench flags
+#   abl:LIB1%LIB2.. bench lines with each library build (--lib; "default" = the shipped one), twice, interleaved
 #   py:SCRIPT,ARGS  python SCRIPT ARGS
 # Outputs: gpurun_out/$TAG/<step index>_<name>.{log,json}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -56,6 +57,13 @@ for step in "$@"; do
            for e in "${ENVS[@]}" "${ENVS[@]}"; do
              rep=$((rep + 1))
              run "ab$(printf %02d $rep)_${e//[^A-Za-z0-9_=]/_}" 300 env ${e//+/ } python bench.py --no-cpu-baseline --no-extra --steps ${STEPS:-100} --warmup 10 $BENCH_ARGS
+           done ;;
+    abl)   IFS='%' read -r -a LIBS <<< "$arg"   # library builds (default = the shipped one), twice, interleaved
+           rep=0
+           for l in "${LIBS[@]}" "${LIBS[@]}"; do
+             rep=$((rep + 1))
+             la=""; [ "$l" != "default" ] && la="--lib $l"
+             run "abl$(printf %02d $rep)_$(basename "$l" .so)" 300 python bench.py --no-cpu-baseline --no-extra --steps ${STEPS:-100} --warmup ${WARM:-50} $la $BENCH_ARGS
            done ;;
     py)    run "py_$(basename "${A[0]}" .py)" 600 python "${A[@]}" ;;
     *) echo "unknown step $step"; exit 2 ;;
