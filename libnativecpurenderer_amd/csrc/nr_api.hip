@@ -358,7 +358,7 @@ void DestroyRenderContext(RenderContext* ctx) {
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     for (auto& F : t.fset) {
-        void* fp[] = {F.fcnt, F.foff, F.fcur, F.fitems, F.frect, F.frec, F.flist, F.dplan, F.gate, F.gplan, F.fperm};
+        void* fp[] = {F.fcnt, F.foff, F.fcur, F.fitems, F.frect, F.frec, F.flist, F.dplan, F.gate, F.gplan};
         for (void* p : fp)
             if (p) NR_CHECK(hipFree(p));
         if (F.h_plan) NR_CHECK(hipHostFree(F.h_plan));

@@ -62,7 +62,6 @@ struct TriScratch {
         uint4* fitems = nullptr; size_t fitems_cap = 0;
         u64* frect = nullptr; size_t frect_cap = 0;   // per-triangle tile rectangle (count -> emit)
         f64* frec = nullptr; size_t frec_cap = 0;     // ordered batches: per-triangle setup records (ORec doubles each)
-        u32* fperm = nullptr; size_t fperm_cap = 0;   // ordered batches: the raster's tile order (k_tile_order)
         u32* flist = nullptr; size_t flist_cap = 0;
         u32* dplan = nullptr;
         u64* h_plan = nullptr;              // pinned, device-mapped copy of the plan totals, (seq << 32) | value

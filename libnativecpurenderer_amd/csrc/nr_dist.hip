@@ -368,6 +368,24 @@ bool frame_u8_local(RenderContext* ctx) {
     return true;
 }
 
+// D2H copy of a frame into pinned host memory by a DMA engine: the pinned
+// buffer's device address as the target of a copy "without compute units".
+// A plain DeviceToHost copy runs as a blit kernel here, which held CU slots
+// for the whole PCIe transfer and slowed the raster beside it about 3x (C2
+// host-delivered kernel trace, profiles/r05/c2_host_trace.txt: k_vis 53 ->
+// 155 us under the copy).  Falls back to the plain copy if the runtime
+// refuses (memory not mapped).
+void copy_to_host_no_cu(void* host, const void* src, size_t n, hipStream_t st) {
+#ifndef NR_D2H_BLIT
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, host, 0) == hipSuccess && dev &&
+        hipMemcpyAsync(dev, src, n, hipMemcpyDeviceToDeviceNoCU, st) == hipSuccess)
+        return;
+    (void)hipGetLastError();
+#endif
+    NR_CHECK(hipMemcpyAsync(host, src, n, hipMemcpyDeviceToHost, st));
+}
+
 }  // namespace
 
 struct NrComm {
@@ -739,8 +757,7 @@ i64 DeliverFrameU8(RenderContext* ctx, iu8* host) {
         NR_CHECK(hipEventRecord(ctx->evFrameReady, ctx->stream));
         NR_CHECK(hipStreamWaitEvent(ctx->commStream, ctx->evFrameReady, 0));
     }   // else: the assembly into x is already queued on the gather stream
-    NR_CHECK(hipMemcpyAsync(host, ctx->frameBuf[x], (size_t)nr_frame_bytes(ctx), hipMemcpyDeviceToHost,
-                            ctx->commStream));
+    copy_to_host_no_cu(host, ctx->frameBuf[x], (size_t)nr_frame_bytes(ctx), ctx->commStream);
     NR_CHECK(hipEventRecord(ctx->evDeliver[x], ctx->commStream));
     if (local) {
         rotate_frame(ctx, x);   // the next frame renders into the other buffer

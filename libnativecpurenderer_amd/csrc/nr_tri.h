@@ -472,11 +472,9 @@ constexpr int ORD_BIN_TILES = 16384;  // tiles of the binned ordered path (the r
 // binned ordered batches: k_tile_sort sorts each tile's list [off[t], off[t + 1])
 // in place (binning stream), then the raster runs one workgroup per tile; both
 // are no-ops unless plan[3] (fits)
-// (and, with perm, writes the raster's tile order: longest list first)
-void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, u32* perm, hipStream_t s,
-                      hipEvent_t stop);
+void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, hipStream_t s, hipEvent_t stop);
 void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* off, const u32* plan, const f64* rec,
-                           const u32* perm, int ntiles, hipStream_t s, hipEvent_t stop);
+                           int ntiles, hipStream_t s, hipEvent_t stop);
 // tb: the batch is that (immutable) TriangleBuffer, so its binning may overlap
 // the previous raster and a repeat draw is sized from its known totals;
 // callerOwned: the arrays are the caller's device memory (DrawTrianglesDevice),

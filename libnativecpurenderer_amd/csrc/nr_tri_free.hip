@@ -1676,16 +1676,12 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     u64* rb[1] = {F.frect};
     if (!grow_set(rb, &F.frect_cap, (size_t)src.n)) return ENQ_FAIL;
     F.frect = rb[0];
-    if (ordered) {   // the ordered raster's per-triangle setup records and tile order
+    if (ordered) {   // the ordered raster's per-triangle setup records
         const size_t need = (size_t)std::max<i64>(src.n, 1) * ORec;
         if (F.frec_cap < need) quiesce();
         f64* rr[1] = {F.frec};
         if (!grow_set(rr, &F.frec_cap, need)) return ENQ_FAIL;
         F.frec = rr[0];
-        if (F.fperm_cap < (size_t)ntiles) quiesce();
-        u32* pr[1] = {F.fperm};
-        if (!grow_set(pr, &F.fperm_cap, (size_t)std::max(ntiles, 1))) return ENQ_FAIL;
-        F.fperm = pr[0];
     }
     size_t cap;
     if (!exact) {
@@ -1810,7 +1806,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     nr_timing_end_on(ctx, NRK_TRI_EMIT, e0, e1, sb);
     if (ordered) {   // each tile's list into submission order
         nr_timing_begin_on(ctx, NRK_TRI_SORT, &e0, &e1, sb);
-        launch_tile_sort(F.foff, F.flist, F.dplan, ntiles, F.fperm, sb, binStop);
+        launch_tile_sort(F.foff, F.flist, F.dplan, ntiles, sb, binStop);
         NR_CHECK(hipGetLastError());
         nr_timing_end_on(ctx, NRK_TRI_SORT, e0, e1, sb);
     }
@@ -1824,7 +1820,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     if (ordered) {   // one workgroup per tile, its list sorted in LDS
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = !e1;
-        launch_ordered_binned(fp, F.flist, F.foff, F.dplan, F.frec, F.fperm, ntiles, sa, vs ? F.evVis : nullptr);
+        launch_ordered_binned(fp, F.flist, F.foff, F.dplan, F.frec, ntiles, sa, vs ? F.evVis : nullptr);
         NR_CHECK(hipGetLastError());
         nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;

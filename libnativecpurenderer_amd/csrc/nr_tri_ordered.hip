@@ -123,12 +123,6 @@ __device__ __forceinline__ u64 window_bits(int xs, int xe) {
     return (n == 64 ? ~0ull : ((1ull << n) - 1ull)) << xs;
 }
 
-#ifndef NR_ORD_FULL
-#define NR_ORD_FULL 1   // (A/B in progress) full units skip their lane-mask loads
-#endif
-#ifndef NR_ORD_LPT
-#define NR_ORD_LPT 1    // (A/B in progress) binned tiles rasterised longest list first
-#endif
 // RGBA: the context has an alpha channel (ipp 4).  An RGB context never
 // stores alpha, so the per-fragment alpha moves are dropped.
 // BINNED: the tile's list comes from the order-free binning, sorted per tile
@@ -142,13 +136,12 @@ template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA, bool BINNED>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 : NR_ORD_WPE))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
                                                     const u32* __restrict__ tstart, const u32* __restrict__ tend,
                                                     const f64* __restrict__ rec, const u32* __restrict__ plan) {
-    if (BINNED && !plan[3]) return;
-    // binned: tend (when given) is the tile order, longest list first (k_tile_order)
-    const int tile = BINNED && tend ? (int)tend[blockIdx.x] : (int)blockIdx.x;
+    const int tile = blockIdx.x;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
     const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
     // (wave: uniform, so the per-wave masks and addresses below stay scalar)
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (BINNED && !plan[3]) return;
     if (!owned_row(ty, fp.period, fp.mask)) return;
     const u32 ls = tstart[tile], le = BINNED ? tstart[tile + 1] : tend[tile];
     if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
@@ -159,10 +152,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
     // exec (it is bound by scalar issue)
     __shared__ __attribute__((aligned(16))) u64 SPM[CH][NWAVE][RPW];
     // span-phase ballots, one per column window q: HITQ[q][w] byte g = which of
-    // triangles 8w..8w+7 touch window q of the tile rows 4g..4g+3, FULLQ[q][w]
-    // byte g = which of them cover every pixel of it
+    // triangles 8w..8w+7 touch window q of the tile rows 4g..4g+3
     __shared__ u64 HITQ[NQ][NWAVE];
-    __shared__ u64 FULLQ[NQ][NWAVE];
     __shared__ iu8 VALID[CH];
     __shared__ iu8 ZPASS[CH];   // depth test known to pass on every covered pixel (see zpass_all)
     __shared__ u32 zmin_w[NWAVE];
@@ -269,9 +260,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
         // wave's ballot per window holds one byte per row group
         {
             const int k = (wave << 3) | (lane & 7), rg = lane >> 3;
-            bool touch[NQ], full[NQ];
+            bool touch[NQ];
 #pragma unroll
-            for (int qq = 0; qq < NQ; ++qq) touch[qq] = full[qq] = false;
+            for (int qq = 0; qq < NQ; ++qq) touch[qq] = false;
             if (k < cnt) {
                 const bool ok = VALID[k];
                 const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
@@ -308,38 +299,30 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
                 const int b = rg / SR;                        // band of these rows
                 const int st0 = ((rg * 4) % (RPW * SR)) / SR; // their first step
 #pragma unroll
-                for (int qq = 0; qq < NQ; ++qq) full[qq] = true;
-#pragma unroll
                 for (int j = 0; j < 4 / SR; ++j)
 #pragma unroll
                     for (int qq = 0; qq < NQ; ++qq) {
                         SPM[k][b * NQ + qq][st0 + j] = mk[j * NQ + qq];
                         touch[qq] |= mk[j * NQ + qq] != 0;
-                        full[qq] &= mk[j * NQ + qq] == ~0ull;
                     }
             }
 #pragma unroll
             for (int qq = 0; qq < NQ; ++qq) {
-                const u64 hit = __ballot(touch[qq]), fl = __ballot(full[qq]);
-                if (lane == 0) { HITQ[qq][wave] = hit; FULLQ[qq][wave] = fl; }
+                const u64 hit = __ballot(touch[qq]);
+                if (lane == 0) HITQ[qq][wave] = hit;
             }
         }
         __syncthreads();
         // this wave's triangles of the chunk (bit k: triangle k touches its
-        // block): the bytes of its band's row groups in its window's ballots;
-        // fm: the triangles covering every pixel of the block (their units
-        // need no lane masks: 43 % of C5's units)
-        constexpr int RGB = RPW * SR / 4;   // 4-row groups per band
-        u64 hm = 0, fm = 0;
+        // block): the bytes of its band's SR row groups in its window's ballots
+        u64 hm = 0;
 #pragma unroll
         for (int w = 0; w < NWAVE; ++w) {
-            const u64 h = uniform_u64(HITQ[q][w]) >> (8 * band * RGB);
-            const u64 f = uniform_u64(FULLQ[q][w]) >> (8 * band * RGB);
-            u64 m = 0, mf = 0xFFull;
+            const u64 h = uniform_u64(HITQ[q][w]) >> (8 * band * SR);
+            u64 m = 0;
 #pragma unroll
-            for (int i = 0; i < RGB; ++i) { m |= h >> (8 * i); mf &= f >> (8 * i); }
+            for (int i = 0; i < SR; ++i) m |= h >> (8 * i);
             hm |= (m & 0xFFull) << (8 * w);
-            fm |= (mf & 0xFFull) << (8 * w);
         }
         // ---- (c) in-order raster of the chunk; each wave owns its block.
         // Every product of the per-pixel expressions that is constant along
@@ -379,15 +362,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
                 const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
                 const f64 fA = RGBA ? S[S_FA][k] : 0.0;
                 u64 lm[RPW];
-                if (NR_ORD_FULL && ((fm >> k) & 1ull)) {   // (scalar branch) every lane of every step covered: no mask loads
-#pragma unroll
-                    for (int r = 0; r < RPW; ++r) lm[r] = ~0ull;
-                } else {
-                    const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
-                    const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
-                    lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
-                    lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
-                }
+                const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
+                const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
+                lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
+                lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
 #endif
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
@@ -547,43 +525,6 @@ __global__ __launch_bounds__(SORT_T) void k_tile_sort(const u32* __restrict__ of
     for (u32 i = tid; i < n; i += SORT_T) list[ls + i] = SL[i];
 }
 
-// The order in which the binned raster takes the tiles: longest list first
-// (a longest-processing-time schedule: C5's 1020 tiles fill its 512
-// workgroup slots about twice, and tiles at the frame's edges hold a quarter
-// of the central ones' triangles).  One workgroup, a counting sort of the list
-// lengths in LDS (length / 16, descending; ties in any order).
-constexpr int ORDER_T = 1024, ORDER_B = 512;
-__global__ __launch_bounds__(ORDER_T) void k_tile_order(const u32* __restrict__ off, int ntiles,
-                                                        u32* __restrict__ perm, const u32* __restrict__ plan) {
-    if (!plan[3]) return;
-    __shared__ u32 hist[ORDER_B];
-    const int tid = threadIdx.x;
-    for (int b = tid; b < ORDER_B; b += ORDER_T) hist[b] = 0;
-    __syncthreads();
-    auto bucket = [&](int t) {   // descending: the longest lists in bucket 0
-        const u32 n = off[t + 1] - off[t];
-        return ORDER_B - 1 - (int)min(n >> 4, (u32)(ORDER_B - 1));
-    };
-    for (int t = tid; t < ntiles; t += ORDER_T) atomicAdd(&hist[bucket(t)], 1u);
-    __syncthreads();
-    if (tid < 64) {   // exclusive scan of the 512 buckets by one wave (8 per lane)
-        u32 v[ORDER_B / 64], s = 0;
-#pragma unroll
-        for (int j = 0; j < ORDER_B / 64; ++j) { v[j] = hist[tid * (ORDER_B / 64) + j]; s += v[j]; }
-        u32 inc = s;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const u32 o = (u32)__shfl_up((int)inc, d, 64);
-            if (tid >= d) inc += o;
-        }
-        u32 e = inc - s;
-#pragma unroll
-        for (int j = 0; j < ORDER_B / 64; ++j) { hist[tid * (ORDER_B / 64) + j] = e; e += v[j]; }
-    }
-    __syncthreads();
-    for (int t = tid; t < ntiles; t += ORDER_T) perm[atomicAdd(&hist[bucket(t)], 1u)] = (u32)t;
-}
-
 template <bool G, bool D, bool C, bool B>
 void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s,
                    const f64* rec, const u32* plan, hipEvent_t stop) {
@@ -607,21 +548,14 @@ void launch_raster_c(const FrameParams& fp, const u32* list, const u32* ts, cons
 
 }  // namespace
 
-void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, u32* perm, hipStream_t s,
-                      hipEvent_t stop) {
-    if (NR_ORD_LPT && perm) {
-        hipLaunchKernelGGL(k_tile_sort, dim3(ntiles), dim3(SORT_T), 0, s, off, list, plan);
-        hipExtLaunchKernelGGL(k_tile_order, dim3(1), dim3(ORDER_T), 0, s, nullptr, stop, 0, off, ntiles, perm, plan);
-    } else {
-        hipExtLaunchKernelGGL(k_tile_sort, dim3(ntiles), dim3(SORT_T), 0, s, nullptr, stop, 0, off, list, plan);
-    }
+void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, hipStream_t s, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(k_tile_sort, dim3(ntiles), dim3(SORT_T), 0, s, nullptr, stop, 0, off, list, plan);
 }
 
 void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* off, const u32* plan, const f64* rec,
-                           const u32* perm, int ntiles, hipStream_t s, hipEvent_t stop) {
-    if (!NR_ORD_LPT) perm = nullptr;
-    if (fp.fragCounter) launch_raster_c<true, true>(fp, list, off, perm, ntiles, s, rec, plan, stop);
-    else launch_raster_c<false, true>(fp, list, off, perm, ntiles, s, rec, plan, stop);
+                           int ntiles, hipStream_t s, hipEvent_t stop) {
+    if (fp.fragCounter) launch_raster_c<true, true>(fp, list, off, nullptr, ntiles, s, rec, plan, stop);
+    else launch_raster_c<false, true>(fp, list, off, nullptr, ntiles, s, rec, plan, stop);
 }
 
 void draw_ordered(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned) {
