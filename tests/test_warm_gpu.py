@@ -58,7 +58,7 @@ def _frames(fac, W, H, scene, nframes, shard=None, inject=None):
         if shard is not None:
             ctx.set_shard(*shard)
         buf = R.TriangleBuffer(xy, c, z=z, gouraud=True)
-    outs = []
+    outs, warm = [], []
     for k in range(nframes):
         if inject is not None and fac.name == "gpu" and k == inject[0]:
             ctx.set_warm_fault_injection(inject[1])
@@ -70,6 +70,9 @@ def _frames(fac, W, H, scene, nframes, shard=None, inject=None):
         else:
             ctx.draw_triangles(xy, c, z=z)
         outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+        if fac.name == "gpu":
+            warm.append(ctx.warm_batch_count())
+    ctx.warm_counts = warm
     return outs, ctx
 
 
@@ -107,8 +110,9 @@ def test_warm_fault_falls_back_exactly(gpu, oracle, mode, mesh_rc):
         assert np.array_equal(g["depth"], o["depth"]), f"frame {k} depth"
     assert ctx.warm_failure_count() == 1
     assert "warm binning" in _lib.last_error(), _lib.last_error()
-    nwarm = ctx.warm_batch_count()
+    w = ctx.warm_counts   # batches binned warm after each frame
+    assert w[3] > w[2], w  # the injected frame was a warm batch
     if mode == 2:
-        assert nwarm >= 4, nwarm   # frames 1-3, and 5-6 once re-captured
+        assert w[6] > w[4], w   # warm again once a cold binning re-captured the schedule
     else:
-        assert nwarm == 3, nwarm   # frames 1-3 only: the buffer bins cold after the failure
+        assert w[6] == w[3], w  # the buffer bins cold after a binning-check failure
