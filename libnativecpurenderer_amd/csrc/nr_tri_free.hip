@@ -50,7 +50,8 @@ namespace {
 constexpr int PROBE_MAX = 65536;
 __device__ unsigned long long nr_probe_buf[PROBE_MAX * 8];
 __device__ unsigned int nr_probe_n;
-__shared__ u64 pr_st[8];   // phase stamps of the current item (thread 0): 1 keys set, 2 raster, 3 merge, 4 hash, 5 records
+__shared__ u64 pr_st[8];   // phase stamps of the current item (thread 0): 1 keys set, 2 raster, 3 merge, 4 hash, 5 records,
+                           // 6 wave 0's first triangle data arrived, 7 wave 0's chunks done (before the barrier)
 #define NR_PROBE_STAMP(k) do { if (threadIdx.x == 0) pr_st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 __device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, int nt) {
     const u32 k = atomicAdd(&nr_probe_n, 1u);
@@ -61,9 +62,9 @@ __device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, in
     e[2] = (u64)d.y | ((u64)d.z << 32);
     auto rel = [&](int q) { return pr_st[q] >= t0 && pr_st[q] <= t1 ? (pr_st[q] - t0) & 0xFFFF : 0xFFFFull; };
     e[4] = rel(1) | (rel(2) << 16) | (rel(3) << 32) | (rel(4) << 48);
-    e[5] = rel(5);
+    e[5] = rel(5) | (rel(6) << 16) | (rel(7) << 32);
     __hip_atomic_store(&e[3], (t1 - t0) | (t0 << 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int q = 1; q < 6; ++q) pr_st[q] = 0;
+    for (int q = 1; q < 8; ++q) pr_st[q] = 0;
 }
 #else
 #define NR_PROBE_STAMP(k) do { } while (0)
@@ -1275,6 +1276,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
             f64 sx[3], sy[3], sl[3];
 #pragma unroll
             for (int v = 0; v < 3; ++v) nr_xform(fp.m, pxy[2 * v], pxy[2 * v + 1], sx[v], sy[v]);
+#if NR_PROBE
+            if (threadIdx.x == 0 && c == (u32)wave) pr_st[6] = __builtin_amdgcn_s_memrealtime() + (sx[0] != sx[0] ? 1 : 0);
+#endif
             const f64 zz0 = hasZ ? pz[0] : 0.0;
             const f64 dz1 = hasZ ? pz[1] - pz[0] : 0.0, dz2 = hasZ ? pz[2] - pz[0] : 0.0;
             pt = ptn;
@@ -1391,6 +1395,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
                 }
             }
         }
+        NR_PROBE_STAMP(7);
         __syncthreads();
         NR_PROBE_STAMP(2);
         if (!multi) {   // the whole list was in this slice: shade now

@@ -80,10 +80,12 @@ starts = np.sort(t0)
 print("item starts at 25/50/75/90/100 %:", " ".join(f"{np.percentile(starts, p):.1f}" for p in (25, 50, 75, 90, 100)))
 
 # phases (thread 0's clock at the barriers): keys set, raster done, merge done (split), hash done, records done, end
-ph = np.stack([((e[:, 4] >> (16 * q)) & 0xFFFF) for q in range(4)] + [e[:, 5] & 0xFFFF], 1).astype(np.float64)
+ph = np.stack([((e[:, 4] >> (16 * q)) & 0xFFFF) for q in range(4)] + [(e[:, 5] >> (16 * q)) & 0xFFFF for q in range(3)],
+              1).astype(np.float64)
 ph[ph == 0xFFFF] = np.nan
+ph[ph == 0] = np.nan
 ph /= 100.0
-names = ["keys", "raster", "merge", "hash", "records"]
+names = ["keys", "raster", "merge", "hash", "records", "w0data", "w0done"]
 print("phase end times (us after item start), mean over items with pairs; single-slice / split-last:")
 single = (L > 0) & (nsl == 1)
 last = (L > 0) & (nsl > 1) & ~np.isnan(ph[:, 3])
