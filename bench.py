@@ -9,11 +9,13 @@ triangles already resident in HBM.  The work unit is a covered on-screen
 pixel x triangle pair (counted once, outside the timed region, by the
 library's fragment counter; equal to the oracle's count — tests check it).
 
-Every step ends with the frame output: the u8 image (cpp:52-57, what the
-video writer consumes) assembled on rank 0.  Multi-GPU (torchrun, one process
-per GPU): the frame's 32-pixel tile rows are owned by the ranks in an
-interleaved pattern; every rank bins and rasterises only its rows (no data-
-path collective), then its rows of the u8 image go to rank 0 as one packed
+Every step ends with the frame output: the frame's YUV420P planes (what the
+video writer's encoder consumes, PutRendererContextFrame cpp:232-275; the u8
+RGB image of cpp:52-57 with --frame-output rgb) assembled on rank 0.
+Multi-GPU (torchrun, one process per GPU): the frame's 32-pixel tile rows are
+owned by the ranks in an interleaved pattern; every rank bins and rasterises
+only its rows (no data-path collective), then its rows of the frame output go
+to rank 0 as one packed
 RCCL message over xGMI, overlapped with the next frame.  Rank 0
 also receives everyone's rows, so its share of the rows is calibrated before
 the timed region (--root-slots auto: candidate weighted patterns timed, the
@@ -413,9 +415,11 @@ def main():
     ap.add_argument("--gloo-test", action="store_true",
                     help="testing the N>1 orchestration on one GPU: gloo process group, CPU reductions, every rank "
                          "renders its shard on its LOCAL_RANK device but the RCCL frame gather is skipped")
-    ap.add_argument("--frame-output", default="rgb", choices=sorted(FRAME_OUT_BPP),
-                    help="frame output of every step: the u8 image (cpp:52-57) or its YUV420P planes (the video "
-                         "encoder's input, PutRendererContextFrame cpp:232-275), written by the raster and gathered")
+    ap.add_argument("--frame-output", default="yuv420p", choices=sorted(FRAME_OUT_BPP),
+                    help="frame output of every step: the YUV420P planes (default since round 5: the video encoder's "
+                         "input, PutRendererContextFrame cpp:232-275 -- 1.5 B/px, which halves the root's ingress "
+                         "at N>1) or the u8 image (cpp:52-57, 3 B/px; the headline's output in rounds 1-4), written "
+                         "by the raster and gathered")
     ap.add_argument("--root-slots", default="auto",
                     help="N>1 (and --emulate-shards): tile-row share of rank 0, in bands per 2 bands of every other "
                          "rank (SetShardSlots); 'equal' = SetShard; 'auto' (N>1) times candidates and keeps the "
@@ -456,8 +460,8 @@ def main():
     do_extra = args.extra if args.extra is not None else (world == 1 and nsh == 1)
     if do_extra and world == 1:
         jobs = [("c3_1080p", "none", None), ("c3_animated", "none", None), ("c2", "none", None), ("c5", "none", None),
-                (args.config, "host", None),
-                (args.config, "host", "yuv420p"), ("c2", "host", None)]
+                (args.config, "none", "rgb"), (args.config, "host", None), (args.config, "host", "rgb"),
+                ("c2", "host", None)]
         for name, dl, fo in jobs:
             if name == args.config and dl == args.deliver and (fo or args.frame_output) == args.frame_output:
                 continue
