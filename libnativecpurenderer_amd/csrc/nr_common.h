@@ -119,7 +119,7 @@ struct TriScratch {
     // warm-batch checks (k_vis WarmCheck): host-mapped word a raster sets when
     // a warm batch failed them (1 binning check, 2 token timeout), read by
     // nr_settle; the batch itself was rasterised from all its triangles
-    u32* hfail = nullptr; u32* dfail = nullptr;
+    u32* hfail = nullptr; u32* dfail = nullptr;   // [0] reason, [1..3] the words it read (the message)
     u32 warmTag = 0;                        // tag of the last warm batch (k_bin_warm's error word)
     u64 warmFailures = 0;                   // warm batches that failed their checks (GetWarmFailureCount)
     std::vector<u64> warmBanned;            // buffers (uid) whose warm binning failed a check: binned cold

@@ -1158,8 +1158,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
         const u32 wt = __hip_atomic_load(&wc.wstat[WS_TAG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const u32 ws = __hip_atomic_load(&wc.wstat[WS_SUM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         fb = !plan[3] || wt == wc.tag || ws != wc.expect;
-        if (fb && blockIdx.x == 0 && threadIdx.x == 0)
-            __hip_atomic_store(wc.hfail, plan[3] ? 1u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (fb && blockIdx.x == 0 && threadIdx.x == 0) {   // (the words read, for the message; then the reason)
+            __hip_atomic_store(&wc.hfail[1], ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&wc.hfail[2], wc.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&wc.hfail[3], (wt == wc.tag ? 1u : 0u) | (plan[3] ? 0u : 2u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&wc.hfail[0], plan[3] ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     } else if (!plan[3]) {
         return;
     }
@@ -1918,14 +1923,21 @@ static void warm_poll(RenderContext* ctx) {
     if (!sc.hfail) return;
     const u32 f = __atomic_load_n(sc.hfail, __ATOMIC_ACQUIRE);
     if (!f) return;
+    const u32 sum = __atomic_load_n(&sc.hfail[1], __ATOMIC_ACQUIRE), want = __atomic_load_n(&sc.hfail[2], __ATOMIC_ACQUIRE);
+    const u32 why = __atomic_load_n(&sc.hfail[3], __ATOMIC_ACQUIRE);
     __atomic_store_n(sc.hfail, 0u, __ATOMIC_RELEASE);
     ++sc.warmFailures;
     if (f == 1 && sc.sched.valid) sc.warmBanned.push_back(sc.sched.tbUid);
     sc.sched.valid = false;
-    nr_set_error_msg(f == 2 ? "triangle batch: a raster's wait for its warm binning timed out; "
-                              "the batch was rasterised from all its triangles"
-                            : "triangle batch: a warm binning failed its range / pair-count check; "
-                              "the batch was rasterised from all its triangles and the buffer bins cold from now on");
+    char msg[320];
+    if (f == 2)
+        snprintf(msg, sizeof msg, "triangle batch: a raster's wait for its warm binning timed out; the batch was "
+                                  "rasterised from all its triangles");
+    else
+        snprintf(msg, sizeof msg, "triangle batch: a warm binning failed its checks (tile over its range: %u, pair "
+                                  "sum %u, expected %u); the batch was rasterised from all its triangles and the "
+                                  "buffer bins cold from now on", why & 1u, sum, want);
+    nr_set_error_msg(msg);
 }
 
 // A warm batch: one binning kernel into the schedule's ranges (binning set
@@ -2041,8 +2053,8 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     TriScratch::FreeSet& F = sc.fset[si];
     if (!F.evBin) { F.evBin = sync_event(); F.evVis = sync_event(); }
     if (!sc.hfail) {
-        NR_CHECK(hipHostMalloc((void**)&sc.hfail, sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
-        *sc.hfail = 0;
+        NR_CHECK(hipHostMalloc((void**)&sc.hfail, 4 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
+        for (int k = 0; k < 4; ++k) sc.hfail[k] = 0;
         NR_CHECK(hipHostGetDevicePointer((void**)&sc.dfail, sc.hfail, 0));
     }
     // cursors [0, ntiles), then the batch checks {error tag, pair sum} (WarmCheck)
