@@ -368,37 +368,6 @@ bool frame_u8_local(RenderContext* ctx) {
     return true;
 }
 
-// D2H copy of a frame into pinned host memory: NR_D2H_WG workgroups, each
-// thread streaming 16-byte vectors into the pinned buffer's device address.
-// The runtime's own DeviceToHost copy is one 512-thread blit workgroup here
-// (no DMA engine on this path, with or without the NoCU flag: kernel traces,
-// round 5), which reached 20-36 GB/s for a 3 MB frame.
-#ifndef NR_D2H_WG
-#define NR_D2H_WG 32
-#endif
-typedef unsigned int nr_u32x4 __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void k_copy_to_host(nr_u32x4* __restrict__ dst, const nr_u32x4* __restrict__ src,
-                                                      i64 n16, iu8* __restrict__ dtail, const iu8* __restrict__ stail,
-                                                      int ntail) {
-    for (i64 i = (i64)blockIdx.x * 256 + threadIdx.x; i < n16; i += (i64)gridDim.x * 256)
-        __builtin_nontemporal_store(src[i], &dst[i]);
-    if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
-}
-void copy_to_host_no_cu(void* host, const void* src, size_t n, hipStream_t st) {
-    void* dev = nullptr;
-    if (NR_D2H_WG > 0 && hipHostGetDevicePointer(&dev, host, 0) == hipSuccess && dev &&
-        ((uintptr_t)dev & 15) == 0 && ((uintptr_t)src & 15) == 0) {
-        const i64 n16 = (i64)(n / 16);
-        const int tail = (int)(n - (size_t)n16 * 16);
-        hipLaunchKernelGGL(k_copy_to_host, dim3(NR_D2H_WG > 0 ? NR_D2H_WG : 1), dim3(256), 0, st, (nr_u32x4*)dev,
-                           (const nr_u32x4*)src, n16, (iu8*)dev + n16 * 16, (const iu8*)src + n16 * 16, tail);
-        NR_CHECK(hipGetLastError());
-        return;
-    }
-    (void)hipGetLastError();
-    NR_CHECK(hipMemcpyAsync(host, src, n, hipMemcpyDeviceToHost, st));
-}
-
 }  // namespace
 
 struct NrComm {
@@ -770,7 +739,10 @@ i64 DeliverFrameU8(RenderContext* ctx, iu8* host) {
         NR_CHECK(hipEventRecord(ctx->evFrameReady, ctx->stream));
         NR_CHECK(hipStreamWaitEvent(ctx->commStream, ctx->evFrameReady, 0));
     }   // else: the assembly into x is already queued on the gather stream
-    copy_to_host_no_cu(host, ctx->frameBuf[x], (size_t)nr_frame_bytes(ctx), ctx->commStream);
+    // (the runtime's copy: one blit workgroup; DMA-engine and wider copy kernels measured slower beside the
+    // raster, profiles/r05/ab_d2h.txt)
+    NR_CHECK(hipMemcpyAsync(host, ctx->frameBuf[x], (size_t)nr_frame_bytes(ctx), hipMemcpyDeviceToHost,
+                            ctx->commStream));
     NR_CHECK(hipEventRecord(ctx->evDeliver[x], ctx->commStream));
     if (local) {
         rotate_frame(ctx, x);   // the next frame renders into the other buffer
