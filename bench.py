@@ -97,6 +97,11 @@ def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True, frame_out="rgb"):
     return int(frac * (n_tri * s_tri + cfg["W"] * cfg["H"] * (8 * 3 + zw + out)))
 
 
+# untimed frames before the warmup steps until the GPU has been under load this
+# long: its clocks ramp for ~30 ms after idle, so a short run (the driver's
+# --warmup 5 --steps 20) would otherwise time part of the ramp (~3-6 %,
+# profiles/r04/warmup_steps20.txt).  Reported as "clock_settle" in the line.
+CLOCK_SETTLE_MS = 60.0
 EVENT_EVERY = 10   # timed-region frames per HIP-event-timed frame of the dominant kernel (each record pair
                    # perturbs the stream: 1 in 4 cost ~7 % of C3 throughput, 1 in 10 ~2 %)
 
@@ -303,6 +308,15 @@ class Runner:
             self.root_k = None if best == "equal" else int(best)
             self.apply_partition(self.root_k)
 
+        # clock settle (CLOCK_SETTLE_MS of frames, untimed), then the W warmup steps
+        self.sync()
+        t0, nset = time.perf_counter(), 0
+        while self.max_over_ranks((time.perf_counter() - t0) * 1e3) < self.args.clock_settle_ms:
+            for i in range(4):   # (every rank the same frames: N > 1 frames end in a collective)
+                self.frame(i)
+            nset += 4
+            self.drain()
+        self.settle_frames = nset
         for i in range(warmup):
             self.frame(i)
         self.drain()
@@ -376,6 +390,7 @@ class Runner:
             "slots": slots,
             "calib": calib,
             "warm_binned_frames": warm_frames,
+            "clock_settle": {"ms": self.args.clock_settle_ms, "frames": self.settle_frames},
         }
         if path == "ordered" and self.cfg.get("soup", (0, 0, None))[2] is not None:
             # C5: the blend loop is bound by f64 VALU issue, not by HBM (per
@@ -394,9 +409,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=200,
-                    help="untimed frames first: the GPU needs ~30 ms of load to reach its steady clocks "
-                         "(10 frames left a 20-step C3 timed region ~3 %% slow, profiles/r04/warmup_steps20.txt)")
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed warmup steps (after the clock settle, --clock-settle-ms)")
+    ap.add_argument("--clock-settle-ms", type=float, default=CLOCK_SETTLE_MS,
+                    help="untimed frames first, until the GPU has rendered this long (its clocks ramp after idle), "
+                         "then the --warmup steps")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", dest="extra", action="store_true", default=None,
@@ -517,6 +534,7 @@ def main():
         "roofline": res["roofline"],
         "raster_path": res["raster_path"],
         "kernel_us": res["kernel_us"],
+        "clock_settle": res["clock_settle"],
         "kernel_us_note": f"per-launch averages from a breakdown pass with events around every kernel; the timed region records events around the dominant kernel on every {EVENT_EVERY}th frame (roofline.kernel_us)",
     }
     if "valu_roofline" in res:

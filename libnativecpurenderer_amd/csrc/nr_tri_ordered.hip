@@ -123,9 +123,6 @@ __device__ __forceinline__ u64 window_bits(int xs, int xe) {
     return (n == 64 ? ~0ull : ((1ull << n) - 1ull)) << xs;
 }
 
-#ifndef NR_ORD_XCD
-#define NR_ORD_XCD 1   // (A/B in progress) XCD-aware tile order
-#endif
 // RGBA: the context has an alpha channel (ipp 4).  An RGB context never
 // stores alpha, so the per-fragment alpha moves are dropped.
 // BINNED: the tile's list comes from the order-free binning, sorted per tile
@@ -139,17 +136,7 @@ template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA, bool BINNED>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 : NR_ORD_WPE))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
                                                     const u32* __restrict__ tstart, const u32* __restrict__ tend,
                                                     const f64* __restrict__ rec, const u32* __restrict__ plan) {
-    // XCD-aware tile order: workgroups are dispatched to the 8 XCDs round robin
-    // (blockIdx % 8), each XCD with its own L2; XCD x takes the x-th eighth of
-    // the tiles in row order, so the tiles in flight on one XCD are a few
-    // neighbouring tile rows and share most of their triangles' setup records
-    // in that XCD's L2 (a C5 triangle lies in ~40 tiles)
-    int tile = blockIdx.x;
-    if (NR_ORD_XCD) {
-        const int per = (int)((gridDim.x + 7) / 8);
-        tile = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-        if (tile >= fp.tiles_x * fp.tiles_y) return;
-    }
+    const int tile = blockIdx.x;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
     const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
     // (wave: uniform, so the per-wave masks and addresses below stay scalar)
@@ -538,19 +525,15 @@ __global__ __launch_bounds__(SORT_T) void k_tile_sort(const u32* __restrict__ of
     for (u32 i = tid; i < n; i += SORT_T) list[ls + i] = SL[i];
 }
 
-// Grid of the tile raster: the XCD-aware order needs a multiple of 8 (the
-// surplus workgroups exit at once).
-static int grid_tiles(int ntiles) { return NR_ORD_XCD ? (ntiles + 7) / 8 * 8 : ntiles; }
-
 template <bool G, bool D, bool C, bool B>
 void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s,
                    const f64* rec, const u32* plan, hipEvent_t stop) {
     if (fp.ipp == 4)
-        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, true, B>), dim3(grid_tiles(ntiles)), dim3(WG), 0, s, nullptr, stop,
-                              0, fp, list, ts, te, rec, plan);
+        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, true, B>), dim3(ntiles), dim3(WG), 0, s, nullptr, stop, 0, fp, list,
+                              ts, te, rec, plan);
     else
-        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, false, B>), dim3(grid_tiles(ntiles)), dim3(WG), 0, s, nullptr,
-                              stop, 0, fp, list, ts, te, rec, plan);
+        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, false, B>), dim3(ntiles), dim3(WG), 0, s, nullptr, stop, 0, fp,
+                              list, ts, te, rec, plan);
 }
 
 template <bool C, bool B>
