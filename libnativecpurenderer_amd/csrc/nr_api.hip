@@ -223,6 +223,7 @@ void nr_ensure_depth(RenderContext* ctx) {
 
 void nr_materialize_color(RenderContext* ctx) {
     nr_settle(ctx);
+    nr_materialize_tiles(ctx, true, false);
     if (!ctx->pendColor) return;
     ctx->pendColor = false;
     ctx->frameU8Valid = false;
@@ -235,6 +236,7 @@ void nr_materialize_color(RenderContext* ctx) {
 
 void nr_materialize_depth(RenderContext* ctx) {
     nr_settle(ctx);
+    nr_materialize_tiles(ctx, false, true);
     if (!ctx->pendDepth) return;
     ctx->pendDepth = false;
     nr_ensure_depth(ctx);
@@ -354,7 +356,7 @@ void DestroyRenderContext(RenderContext* ctx) {
     TriScratch& t = ctx->tri;
     void* ptrs[] = {ctx->buffer, ctx->depth, t.cnt,  t.off,        t.keys[0], t.keys[1], t.vals[0],
                     t.vals[1],   t.tile_start, t.tile_end, t.temp, t.stage, t.d_frag, t.d_flag, ctx->u8buf,
-                    t.fdone,     t.kslot, t.orec};
+                    t.fdone,     t.kslot, t.orec, ctx->tileStamp};
     for (void* p : ptrs)
         if (p) NR_CHECK(hipFree(p));
     for (auto& F : t.fset) {
@@ -402,6 +404,7 @@ void ResizeRenderContext(RenderContext* ctx, i64 width, i64 height) {
         nr_set_error_msg("ResizeRenderContext: odd size, frame output format reset from YUV420P to the u8 image");
     }
     ctx->pendColor = ctx->pendDepth = false;
+    ctx->tileColor = ctx->tileDepth = false;
     i64 n = GetBufferSize(ctx);
     NR_CHECK(hipMalloc(&ctx->buffer, (size_t)(n > 0 ? n : 1) * sizeof(f64)));
     NR_CHECK(hipMemsetAsync(ctx->buffer, 0, (size_t)(n > 0 ? n : 1) * sizeof(f64), ctx->stream));
@@ -674,9 +677,11 @@ void SetColor(RenderContext* ctx, f64 r, f64 g, f64 b, f64 a) {
         // uniform clear: kept pending, consumed on chip by the tiled raster
         ctx->pendColor = true;
         ctx->pendColorValue = r;
+        ctx->tileColor = false;   // (superseded)
         return;
     }
     ctx->pendColor = false;   // fully overwritten
+    ctx->tileColor = false;
     int ipp = ctx->enableAlpha ? 4 : 3;
     i64 n = ctx->width * ctx->height;
     if (n <= 0) return;

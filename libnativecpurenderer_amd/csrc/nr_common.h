@@ -147,6 +147,15 @@ struct RenderContext {
     // other operation that touches the buffer.
     bool pendColor = false; f64 pendColorValue = 0;
     bool pendDepth = false; u32 pendDepthValue = 0xFFFFFFFFu;
+    // tile-granular pending clears (a fast clear): an order-free batch that
+    // consumed a pending clear leaves the tiles no triangle touched holding it
+    // in name only -- their framebuffer / depth pixels are not written; tile t
+    // is such a tile while tileStamp[t] == tileEpoch (written by k_vis).  Any
+    // later use of the buffers writes them first (nr_materialize_tiles), a new
+    // clear of the same buffer drops them.
+    bool tileColor = false; f64 tileColorValue = 0;
+    bool tileDepth = false; u32 tileDepthValue = 0xFFFFFFFFu;
+    u32* tileStamp = nullptr; i64 tileStampCap = 0; u32 tileEpoch = 0;
     TriScratch tri;
     // per-kernel HIP-event timing (bench.py's live roofline measurement)
     bool timing = false;
@@ -240,6 +249,7 @@ void nr_timing_end_on(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b, h
 void nr_materialize(RenderContext* ctx);          // flush pending clears
 void nr_materialize_color(RenderContext* ctx);
 void nr_materialize_depth(RenderContext* ctx);
+void nr_materialize_tiles(RenderContext* ctx, bool color, bool depth);   // tile-granular pending clears
 void nr_ensure_depth(RenderContext* ctx);
 void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
 void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);

@@ -318,7 +318,7 @@ void rotate_frame(RenderContext* ctx, int x) {
 // The u8 image of the owned bands (the first half of GatherFrameU8), converted
 // only when the mirror the resolves write is not current.
 bool frame_u8_local(RenderContext* ctx) {
-    nr_materialize_color(ctx);
+    nr_settle(ctx);   // (the buffer's pending clears are written only if the f64 frame is converted below)
     const int ipp = ctx->enableAlpha ? 4 : 3;
     const i64 n = nr_frame_bytes(ctx);
     if (n <= 0) return true;
@@ -348,6 +348,7 @@ bool frame_u8_local(RenderContext* ctx) {
     // of the f64 frame); convert here only when that mirror is not current
     ctx->frameOutput = true;
     if (owned > 0 && !ctx->frameU8Valid) {
+        nr_materialize_color(ctx);
         hipEvent_t e0, e1;
         nr_timing_begin(ctx, NRK_OUTPUT, &e0, &e1);
         if (ctx->frameFormat == 1) {

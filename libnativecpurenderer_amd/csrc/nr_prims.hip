@@ -530,6 +530,7 @@ void nr_flush_commands(RenderContext* ctx) {
     // pageable source: the copy is staged before the call returns, so the
     // vector can be reused at once
     NR_CHECK(hipMemcpyAsync(L->dev, L->cmds.data(), n * sizeof(NrCmd), hipMemcpyHostToDevice, ctx->stream));
+    nr_materialize_tiles(ctx, true, false);
     const int pend = ctx->pendColor ? 1 : 0;
     const f64 pv = ctx->pendColorValue;
     ctx->pendColor = false;   // the launch writes every pixel when a clear is pending

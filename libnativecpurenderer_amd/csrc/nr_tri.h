@@ -351,6 +351,8 @@ struct FrameParams {
     iu8* frameU8;                      // non-null: resolve also writes the frame output: the u8
                                        // image (cpp:52-57), or with frameYUV its YUV420P planes
     int frameYUV;
+    u32* tileStamp;   // non-null: k_vis leaves an empty tile's pending clears pending (stamps it tileEpoch,
+    u32 tileEpoch;    // RenderContext::tileStamp) and writes only its frame output
 };
 
 // Frame output of pixel p = (px, py) from its framebuffer value, written by
@@ -456,6 +458,7 @@ bool grow_temp(TriScratch& sc, size_t need);
 
 FrameParams frame_params(RenderContext* ctx, const TriSrc& src);
 void finish_batch(RenderContext* ctx, const FrameParams& fp);
+u32* tile_stamps(RenderContext* ctx, i64 ntiles);   // the context's tile stamps, next epoch (nr_tri.hip)
 
 // the two rasterisers (host side)
 // ordered batches: binned like the order-free ones (count / plan / emit, on the

@@ -32,6 +32,7 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src) {
     TriScratch& sc = ctx->tri;
     if (!sc.h_total) NR_CHECK(hipHostMalloc((void**)&sc.h_total, 4 * sizeof(u64)));
     if (ctx->depthTest) nr_ensure_depth(ctx);
+    nr_materialize_tiles(ctx, true, true);   // (a batch starts from whole-frame clear state)
     FrameParams fp;
     fp.src = src;
     for (int k = 0; k < 6; ++k) fp.m[k] = ctx->m[k];
@@ -54,6 +55,8 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src) {
     fp.fragCounter = nullptr;
     fp.frameU8 = nullptr;
     fp.frameYUV = ctx->frameFormat == 1;
+    fp.tileStamp = nullptr;
+    fp.tileEpoch = 0;
     if (ctx->countFragments) {
         if (!sc.d_frag) NR_CHECK(hipMalloc(&sc.d_frag, sizeof(u64)));
         NR_CHECK(hipMemsetAsync(sc.d_frag, 0, sizeof(u64), ctx->stream));
@@ -73,8 +76,50 @@ void finish_batch(RenderContext* ctx, const FrameParams& fp) {
         NR_CHECK(hipStreamSynchronize(ctx->stream));
         ctx->fragTotal += sc.h_total[2];
     }
+    if (fp.tileStamp) {   // the empty tiles' clears stay pending (k_vis stamped them)
+        ctx->tileColor = fp.pendColor != 0;
+        ctx->tileColorValue = fp.pendColorValue;
+        ctx->tileDepth = fp.pendDepth != 0;
+        ctx->tileDepthValue = fp.pendDepthValue;
+    }
     ctx->pendColor = false;
     if (ctx->depthTest) ctx->pendDepth = false;
+}
+
+namespace {
+
+// Writes the pending clears of the tiles stamped `epoch` (one workgroup per tile).
+__global__ __launch_bounds__(256) void k_tile_clear(f64* __restrict__ fb, u32* __restrict__ depth, i64 W, i64 H,
+                                                    int tiles_x, int ipp, const u32* __restrict__ stamp, u32 epoch,
+                                                    int doColor, f64 cv, int doDepth, u32 dv) {
+    const int tile = blockIdx.x;
+    if (stamp[tile] != epoch) return;
+    const i64 x0 = (i64)(tile % tiles_x) * TW, y0 = (i64)(tile / tiles_x) * TH;
+    for (int p = threadIdx.x; p < TW * TH; p += 256) {
+        const i64 px = x0 + (p & (TW - 1)), py = y0 + p / TW;
+        if (px >= W || py >= H) continue;
+        const i64 q = py * W + px;
+        if (doColor)
+            for (int c = 0; c < ipp; ++c) fb[q * ipp + c] = cv;
+        if (doDepth) depth[q] = dv;
+    }
+}
+
+}  // namespace
+
+// Stamp array of at least `ntiles` entries (zero = no epoch).
+u32* tile_stamps(RenderContext* ctx, i64 ntiles) {
+    if (ctx->tileStampCap < ntiles) {
+        if (ctx->tileStamp) NR_CHECK(hipFree(ctx->tileStamp));
+        NR_CHECK(hipMalloc(&ctx->tileStamp, (size_t)ntiles * sizeof(u32)));
+        NR_CHECK(hipMemsetAsync(ctx->tileStamp, 0, (size_t)ntiles * sizeof(u32), ctx->stream));
+        ctx->tileStampCap = ntiles;
+    }
+    if (++ctx->tileEpoch == 0) {   // (wrapped: no stale stamp may equal a new epoch)
+        NR_CHECK(hipMemsetAsync(ctx->tileStamp, 0, (size_t)ctx->tileStampCap * sizeof(u32), ctx->stream));
+        ctx->tileEpoch = 1;
+    }
+    return ctx->tileStamp;
 }
 
 namespace {
@@ -156,6 +201,22 @@ void draw(RenderContext* ctx, const f64* xy, const f64* z, const f64* rgba, i64 
 
 using namespace nrtri;
 
+void nr_materialize_tiles(RenderContext* ctx, bool color, bool depth) {
+    const bool c = color && ctx->tileColor, d = depth && ctx->tileDepth && ctx->depth;
+    if (!c && !d) return;
+    if (c) ctx->tileColor = false;
+    if (d) ctx->tileDepth = false;
+    const i64 tx = (ctx->width + TW - 1) / TW, ty = (ctx->height + TH - 1) / TH;
+    if (tx * ty <= 0) return;
+    hipEvent_t a, b;
+    nr_timing_begin(ctx, NRK_FILL, &a, &b);
+    hipLaunchKernelGGL(k_tile_clear, dim3((unsigned)(tx * ty)), dim3(256), 0, ctx->stream, ctx->buffer, ctx->depth,
+                       ctx->width, ctx->height, (int)tx, ctx->enableAlpha ? 4 : 3, ctx->tileStamp, ctx->tileEpoch,
+                       c ? 1 : 0, ctx->tileColorValue, d ? 1 : 0, ctx->tileDepthValue);
+    NR_CHECK(hipGetLastError());
+    nr_timing_end(ctx, NRK_FILL, a, b);
+}
+
 void nr_settle(RenderContext* ctx) {
     nrtri::settle(ctx);
     nr_flush_commands(ctx);   // recorded draws come after the last batch in program order
@@ -173,6 +234,7 @@ void SetDepthState(RenderContext* ctx, bool test, bool write) {
 void ClearDepth(RenderContext* ctx, u32 value) {
     ctx->pendDepth = true;
     ctx->pendDepthValue = value;
+    ctx->tileDepth = false;   // (superseded)
 }
 
 // New: copy the W*H u32 depth buffer to the host.

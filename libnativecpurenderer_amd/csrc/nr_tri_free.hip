@@ -70,6 +70,12 @@ __device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, in
 #define NR_PROBE_STAMP(k) do { } while (0)
 #endif
 
+// Fast clear (RenderContext::tileStamp): 0 = empty tiles write their pending
+// clears in k_vis (A/B).
+#ifndef NR_FAST_CLEAR
+#define NR_FAST_CLEAR 1
+#endif
+
 constexpr int VWG = 256;  // k_vis workgroup
 // k_vis occupancy: 4 waves per SIMD (<= 128 VGPRs, and LDS <= 40 KB per
 // workgroup: 280 shading records over the keys + REC_EXTRA) measured 6-10 %
@@ -1215,6 +1221,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
         const int hlim = (int)(fp.H - y0 < TH ? fp.H - y0 : TH);
         const int rcap = hlim;   // rows [rlo, rcap) of the tile are rasterised here
         if (ls == le && !multi) {   // no triangle: only the pending clears
+            if (fp.tileStamp) {
+                // fast clear: the tile's framebuffer and depth keep the clear
+                // pending (RenderContext::tileStamp); only the frame output,
+                // which the batch hands over, is written
+                if (fp.frameU8 && fp.pendColor) {
+                    const f64 v = fp.pendColorValue;
+                    for (int p = itid; p < TH * TW; p += NT) {
+                        const int lx = p & (TW - 1), ly = p / TW;
+                        if (lx < wlim && ly < hlim)
+                            store_frame_out(fp, (y0 + ly) * fp.W + x0 + lx, x0 + lx, y0 + ly, v, v, v, v);
+                    }
+                }
+                if (itid == 0) fp.tileStamp[tile] = fp.tileEpoch;
+                continue;
+            }
             for (int p = itid; p < TH * TW; p += NT) {
                 const int lx = p & (TW - 1), ly = p / TW;
                 if (lx < wlim && ly < hlim)
@@ -2175,6 +2196,8 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         const size_t n = (size_t)nr_frame_bytes(ctx);
         if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
     }
+    if (!ordered && (fp.pendColor || fp.pendDepth) && NR_FAST_CLEAR)   // (k_vis: empty tiles' clears stay pending)
+        fp.tileStamp = tile_stamps(ctx, (i64)fp.tiles_x * fp.tiles_y), fp.tileEpoch = ctx->tileEpoch;
     BinParams bp;
     bp.src = src;
     for (int k = 0; k < 6; ++k) bp.m[k] = ctx->m[k];
@@ -2242,6 +2265,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
                                ordered);
     if (r == ENQ_FAIL) return;
     if (r == ENQ_SORTED) {   // (exact) a tile list too long for the LDS sort
+        fp.tileStamp = nullptr;   // (the ordered raster writes every tile)
         draw_ordered_sorted(ctx, src, fp, bp);
         return;
     }
