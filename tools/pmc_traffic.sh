@@ -11,6 +11,6 @@ mkdir -p $OUT
 KR=${KERNEL_REGEX:-"k_vis|k_tile_raster"}
 for c in FETCH_SIZE WRITE_SIZE; do
   NR_WARM_INLINE=1 timeout -k 10 240 rocprofv3 --pmc $c --kernel-include-regex "$KR" -d $OUT/$c -o run --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --no-extra --steps 3 --warmup 1 $ARGS > $OUT/$c.log 2>&1 || { echo "pmc $c rc=$?"; tail -5 $OUT/$c.log; exit 1; }
+    python3 bench.py --no-cpu-baseline --no-extra --steps 3 --warmup 1 --clock-settle-ms 0 $ARGS > $OUT/$c.log 2>&1 || { echo "pmc $c rc=$?"; tail -5 $OUT/$c.log; exit 1; }
 done
 python tools/pmc_json.py $OUT $TAG "$ARGS"
