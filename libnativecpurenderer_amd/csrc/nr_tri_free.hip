@@ -1874,13 +1874,16 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
 static bool warm_on(const TriScratch& sc) { return sc.warmMode != 2; }
 // Warm binning inline (main stream, right before the raster) or beside the
 // previous raster (binning stream).  Inline when the rank's owned share of
-// the batch is large: 1M triangles unsharded 0.154 -> 0.140 ms per frame,
-// neutral at 2 shards; beside the raster for small batches (C2 0.065 ->
-// 0.058 ms) and for the smaller shares, whose active binning blocks fit
+// the batch is large and its frame share small: 1M triangles at 1080p
+// 0.1001 -> 0.0985 ms per frame; beside the raster for small batches (C2
+// 0.065 -> 0.058 ms), for the smaller shares, whose active binning blocks fit
 // beside the raster (8-way 0.0505 -> 0.046-0.048 ms, 4-way -1 %;
-// profiles/r04/ab_warm_blocks.txt).  NR_WARM_INLINE: 1 always inline, 0
+// profiles/r04/ab_warm_blocks.txt), and -- since the fast clear left the
+// raster HBM time to share -- for frame shares of >= 4 M pixels (C3 at 4K
+// 0.130 -> 0.124 ms, its 2-way share 0.092 -> 0.077 ms;
+// profiles/r05/ab_warm_beside.txt).  NR_WARM_INLINE: 1 always inline, 0
 // always beside (A/B).
-static bool warm_inline(i64 n, int period, u64 mask) {
+static bool warm_inline(i64 n, int period, u64 mask, i64 W, i64 H) {
     static const int v = [] {
         const char* e = getenv("NR_WARM_INLINE");
         return e ? atoi(e) : 2;
@@ -1888,6 +1891,7 @@ static bool warm_inline(i64 n, int period, u64 mask) {
     if (v != 2) return v != 0;
     const u64 m = period >= 64 ? mask : (mask & ((1ull << period) - 1ull));
     const f64 share = period == 1 ? 1.0 : (f64)__builtin_popcountll(m) / (f64)period;
+    if ((f64)W * (f64)H * share >= 4.0e6) return false;
     return n >= 65536 && (f64)n * share >= 300000.0;
 }
 
@@ -2067,7 +2071,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     TriScratch& sc = ctx->tri;
     auto& S = sc.sched;
     hipStream_t sa = ctx->stream;
-    hipStream_t sb = warm_inline(bp.src.n, fp.period, fp.mask) ? sa : nr_bin_stream_for(ctx->device);
+    hipStream_t sb = warm_inline(bp.src.n, fp.period, fp.mask, fp.W, fp.H) ? sa : nr_bin_stream_for(ctx->device);
     const int ntiles = fp.tiles_x * fp.tiles_y;
     const int si = sc.fnext;
     sc.fnext = (sc.fnext + 1) % BIN_SETS;
