@@ -35,10 +35,7 @@ constexpr int CH = 64;           // triangles staged per chunk
 // (C5 k_tile_raster): 778 us at 64 x 4, 715 us at 32 x 8, 746 us at 16 x 16 (its
 // masks take four window ballots and more span-phase work per chunk), so 32 x 8
 // (profiles/r03_c5/ab_blocks.txt).
-#ifndef NR_ORD_BW
-#define NR_ORD_BW 32
-#endif
-constexpr int BW = NR_ORD_BW;    // block columns (64, 32 or 16)
+constexpr int BW = 32;           // block columns (64, 32 and 16 measured)
 constexpr int SR = 64 / BW;      // rows per step
 constexpr int NQ = TW / BW;      // column windows of the tile
 static_assert(BW * SR == 64 && NQ * (TH / (RPW * SR)) == NWAVE, "wave blocks tile the tile");
@@ -129,11 +126,9 @@ __device__ __forceinline__ u64 window_bits(int xs, int xe) {
 // by k_tile_sort (tstart = the plan's list offsets: [off[tile], off[tile + 1]));
 // the batch is a no-op unless plan[3] (fits); otherwise [tstart, tend) of the
 // globally sorted pairs.
-#ifndef NR_ORD_WPE
-#define NR_ORD_WPE 4   // 6 (80 VGPRs, 85 spilled): C5 raster 740 -> 1355 us
-#endif
+// 4 waves per SIMD (6: 80 VGPRs, 85 spilled -- C5 raster 740 -> 1355 us)
 template <bool GOURAUD, bool DEPTH, bool COUNT, bool RGBA, bool BINNED>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 : NR_ORD_WPE))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile_raster(const FrameParams fp, const u32* __restrict__ list,
                                                     const u32* __restrict__ tstart, const u32* __restrict__ tend,
                                                     const f64* __restrict__ rec, const u32* __restrict__ plan) {
     const int tile = blockIdx.x;
@@ -275,21 +270,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
                 u64 mk[RPW];   // [j * NQ + qq]: step (4 rg % (RPW SR)) / SR + j of window qq
 #pragma unroll
                 for (int i = 0; i < RPW; ++i) mk[i] = 0;
-#ifndef NR_ORD_SPAN32
-#define NR_ORD_SPAN32 0   // 1: measured slower on C5 (786 vs 740 us, profiles/r03_c5/ab_span32_wpe.txt)
-#endif
-                // f32 crossings with an error bound (row_span32, as k_vis), the
-                // exact f64 statement for the rows the bound cannot decide
-                Span32 S32;
-                if (NR_ORD_SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);
+                // (f32 row spans as in k_vis measured slower here: 786 vs 740 us,
+                // profiles/r03_c5/ab_span32_wpe.txt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = rg * 4 + r;
                     const i64 gy = y0 + row;
                     int xs = 0, xe = 0;
                     if (ok && gy < fp.H && ymn <= (f64)gy && (f64)gy < ymx) {
-                        if (!NR_ORD_SPAN32 || !row_span32(S32, row, (f64)gy, (float)wlim, xs, xe))
-                            row_span_slopes(sx, sy, sl, (f64)gy, (f64)x0, wlim, xs, xe);
+                        row_span_slopes(sx, sy, sl, (f64)gy, (f64)x0, wlim, xs, xe);
                     }
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
 #pragma unroll
@@ -337,28 +326,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
             // this wave's block
             for (; hm; hm &= hm - 1) {
                 const int k = (int)__builtin_ctzll(hm);
-#ifndef NR_ORD_L0
-#define NR_ORD_L0 0   // A/B: the unit's masks and blend terms read by lane 0 only (LDS bytes / 64), then readfirstlane
-#endif
-#if NR_ORD_L0
-                u64 lm[RPW];
-                f64 om, RA, GA, BA, fA = 0.0;
-                {
-                    ulonglong2 m01 = make_ulonglong2(0, 0), m23 = make_ulonglong2(0, 0);
-                    f64 t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-                    if (lane == 0) {
-                        m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
-                        m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
-                        t0 = S[S_OM][k]; t1 = S[S_RA][k]; t2 = S[S_GA][k]; t3 = S[S_BA][k];
-                        if (RGBA) t4 = S[S_FA][k];
-                    }
-                    lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
-                    lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
-                    auto uf = [](f64 v) { return __longlong_as_double((long long)uniform_u64((u64)__double_as_longlong(v))); };
-                    om = uf(t0); RA = uf(t1); GA = uf(t2); BA = uf(t3);
-                    if (RGBA) fA = uf(t4);
-                }
-#else
                 const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
                 const f64 fA = RGBA ? S[S_FA][k] : 0.0;
                 u64 lm[RPW];
@@ -366,7 +333,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GOURAUD ? 4 
                 const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
                 lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
                 lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
-#endif
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
                     if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
