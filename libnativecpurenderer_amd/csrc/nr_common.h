@@ -339,6 +339,26 @@ __device__ __forceinline__ u32 nr_quantize_depth_bl(f64 z) {
     return (u32)fmin(fmax(z * 4294967295.0, 0.0), 4294967295.0);
 }
 
+// The same function in one conversion: gfx950's v_cvt_u32_f64 truncates and
+// saturates (negative and -inf to 0, >= 2^32 and +inf to 0xFFFFFFFF, NaN to
+// 0), which is exactly the clamp above -- two f64 VALU operations fewer per
+// fragment.  (In C++ an out-of-range cast is undefined, hence the asm.)
+// Pinned against nr_quantize_depth on NaN, infinities, huge and boundary
+// values by tests/test_depth_edges_gpu.py.
+#ifndef NR_QUANT_HW
+#define NR_QUANT_HW 1
+#endif
+__device__ __forceinline__ u32 nr_quantize_depth_hw(f64 z) {
+#if NR_QUANT_HW
+    const f64 p = z * 4294967295.0;
+    u32 r;
+    asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(p));
+    return r;
+#else
+    return nr_quantize_depth_bl(z);
+#endif
+}
+
 // Bytes of the context's frame output (frameFormat: u8 image or YUV420P).
 static inline i64 nr_frame_bytes(const RenderContext* ctx) {
     const i64 W = ctx->width, H = ctx->height;

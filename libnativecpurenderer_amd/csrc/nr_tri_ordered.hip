@@ -412,7 +412,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 u32 zq = 0;
                 if (ztest) {
                     const f64 zz = S[S_Z0][k] + S[S_DZ1][k] * w1 + S[S_DZ2][k] * w2;
-                    zq = nr_quantize_depth(zz);
+                    zq = nr_quantize_depth_hw(zz);
                     if (!(zq < cz[r])) continue;
                 }
                 if (GOURAUD) {

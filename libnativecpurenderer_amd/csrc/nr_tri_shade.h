@@ -155,7 +155,7 @@ __device__ __forceinline__ u32 frag_depth(f64 X, f64 dy, f64 sx0, f64 e1x, f64 e
     const f64 w1 = (dx * e2y - e2x * dy) * inv;
     const f64 w2 = (e1x * dy - dx * e1y) * inv;
     const f64 zz = zz0 + dz1 * w1 + dz2 * w2;
-    return nr_quantize_depth_bl(zz);
+    return nr_quantize_depth_hw(zz);
 }
 // ... into the tile's LDS keys (k_vis).
 template <int ZMODE>
