@@ -89,8 +89,8 @@ PATCHES = {
          "        atomicAdd(&g_acc[5], sh_t4 - sh_t3); atomicAdd(&g_acc[3], 1ull); atomicAdd(&g_acc[4], (u64)nU); }\n}\n"),
     ],
     "EXP_NOROWS": [
-        ("            if (r0 >= r1) continue;\n",
-         "            if (r0 >= r1) continue;\n            if (EXP_NOROWS) { if (r1 > 1000) key[0] = r0; continue; }\n"),
+        ("            if (r0 < r1 && !big) {\n",
+         "            if (EXP_NOROWS && r0 < r1 && !big) { if (r1 > 1000) key[0] = r0; }\n            else if (r0 < r1 && !big) {\n"),
     ],
     "EXP_NOPIX": [
         ("                    if (xs >= xe) continue;\n                    if (ZMODE == 0) {",
