@@ -80,7 +80,7 @@ constexpr int VWG = 256;  // k_vis workgroup
 // k_vis occupancy: 4 waves per SIMD (<= 128 VGPRs, and LDS <= 40 KB per
 // workgroup: 280 shading records over the keys + REC_EXTRA) measured 6-10 %
 // faster on C3 than 3 (135 VGPRs, 53.5 KB); k_vis is latency-bound.
-constexpr int VIS_WPE = 4;
+constexpr int VIS_WPE = 4;   // (5 waves: 96 VGPRs + 112 B spills, C3 +16 %, profiles/r05/ab_vis_occupancy.txt)
 constexpr u32 SLICE = 1024;      // longest work item (triangles)
 constexpr u32 SLICE_MIN = 64;    // shortest slice of a split tile
 // Items the plan kernel aims for when it picks the slice length.  Round 4
