@@ -217,6 +217,21 @@ class Runner:
         if deliver == "host":
             nbytes = int(np.prod(self.ctx.frame_output_shape()))
             self.host = [R.HostBuffer(nbytes) for _ in range(2)]
+        elif deliver == "bands":
+            # every rank copies its own bands into one host frame (two, in
+            # turn): shared pinned memory across the ranks' processes at N > 1
+            nbytes = int(np.prod(self.ctx.frame_output_shape()))
+            if world > 1:
+                tag = os.environ.get("MASTER_PORT", "0")
+                names = [f"/nr_bench_frame{j}_{tag}" for j in range(2)]
+                if rank == 0:
+                    self.host = [R.SharedHostBuffer(nm, nbytes, owner=True) for nm in names]
+                dist.barrier()
+                if rank != 0:
+                    self.host = [R.SharedHostBuffer(nm, nbytes) for nm in names]
+                dist.barrier()
+            else:
+                self.host = [R.HostBuffer(nbytes) for _ in range(2)]
         self.fixed_k = None if args.root_slots in ("auto", "equal") else int(args.root_slots)
         self.root_k = self.fixed_k
         self.apply_partition(self.fixed_k)
@@ -244,6 +259,13 @@ class Runner:
             ctx.restore_state()
         else:
             ctx.draw_triangle_buffer(self.buf)
+        if self.deliver == "bands":
+            # no gather: this rank's bands straight into the host frame; host
+            # frame i % 2 is rewritten only after frame i-2's copies landed
+            if len(self.tickets) >= 2:
+                ctx.wait_frame_delivered(self.tickets.pop(0))
+            self.tickets.append(ctx.deliver_frame_bands(self.host[i % 2]))
+            return
         ctx.gather_frame_u8(self.comm, 0)
         if self.host is not None and self.rank == 0:
             # frame i's D2H runs on the gather stream while frame i+1 renders;
@@ -420,9 +442,11 @@ def main():
                     help="also time the metric's literal config (1M tris at 1080p), c2, c5 and host-delivered "
                          "frames, reported under 'extra' (default at N=1)")
     ap.add_argument("--no-extra", dest="extra", action="store_false")
-    ap.add_argument("--deliver", default="none", choices=("none", "host"),
+    ap.add_argument("--deliver", default="none", choices=("none", "host", "bands"),
                     help="host: every step ends with the frame output on the host (pinned buffers, D2H of frame k "
-                         "overlapped with frame k+1), as the video caller (PutRendererContextFrame) needs it")
+                         "overlapped with frame k+1), as the video caller (PutRendererContextFrame) needs it; "
+                         "bands: every rank copies its own bands straight into one shared pinned host frame "
+                         "(DeliverFrameBands, no GPU gather: each GPU's PCIe link carries its share)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
     ap.add_argument("--lib", default=None,
@@ -525,8 +549,10 @@ def main():
         "config": {"workload": cfg["desc"], "width": run.W, "height": run.H, "triangles": run.n_tri,
                    "fragments_per_frame": res["fragments_per_frame"], "frame_pixels": run.W * run.H,
                    "frame_output": args.frame_output,
-                   "frame_delivery": "host (pinned, D2H overlapped)" if args.deliver == "host" else "in HBM",
-                   "parallelism": (f"tile-row shards x{world} + RCCL u8 frame gather" if world > 1
+                   "frame_delivery": {"host": "host (pinned, D2H overlapped)",
+                                      "bands": "host, each rank's own bands into one shared pinned host frame "
+                                               "(DeliverFrameBands, no gather)"}.get(args.deliver, "in HBM"),
+                   "parallelism": (f"tile-row shards x{world} + " + ("bands into a shared host frame" if args.deliver == "bands" else "RCCL u8 frame gather") if world > 1
                                    else f"EMULATED shard 0 of {nsh} on one GPU (no gather)" if nsh > 1
                                    else "single GPU"),
                    **({"shard_slots": res["slots"] or "equal", "partition_calibration_ms": res["calib"]}

@@ -174,6 +174,14 @@ i64 DeliverFrameU8(RenderContext* ctx, iu8* host);  /* async D2H of that frame i
 bool WaitFrameDelivered(RenderContext* ctx, i64 ticket);
 void* AllocHostBuffer(i64 bytes);                   /* pinned host memory (DeliverFrameU8 targets) */
 void FreeHostBuffer(void* p);
+i64 DeliverFrameBands(RenderContext* ctx, iu8* host); /* §8e: this rank's bands of its frame output straight into
+                                                       their places in a host frame (every rank into the same one:
+                                                       assembled by each GPU's own PCIe link, no GPU ingress);
+                                                       async on the gather stream -> ticket for WaitFrameDelivered */
+void* AllocSharedHostBuffer(const char* name, i64 bytes); /* pinned POSIX shared memory "/name" (one host frame for
+                                                       the processes of a sharded frame) */
+void FreeSharedHostBuffer(void* p, i64 bytes);
+bool UnlinkSharedHostBuffer(const char* name);
 bool SetFrameFormat(RenderContext* ctx, i64 format); /* 0: u8 image (default), 1: YUV420P planes written by the
                                                        raster and gathered as such (W, H even; same on all ranks) */
 i64 GetFrameFormat(RenderContext* ctx);

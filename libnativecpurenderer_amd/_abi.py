@@ -112,6 +112,10 @@ DEVICE_ABI = {
     "WaitFrameDelivered": (B, (P, L)),
     "AllocHostBuffer": (P, (L,)),
     "FreeHostBuffer": (None, (P,)),
+    "DeliverFrameBands": (L, (P, P)),
+    "AllocSharedHostBuffer": (P, (ctypes.c_char_p, L)),
+    "FreeSharedHostBuffer": (None, (P, L)),
+    "UnlinkSharedHostBuffer": (B, (ctypes.c_char_p,)),
     "GetFrameYUV420P": (B, (P, P)),
     "SetFrameFormat": (B, (P, L)),
     "GetFrameFormat": (L, (P,)),

@@ -14,6 +14,10 @@
 // RCCL is bound at run time with dlopen/dlsym, so the library loads (and the
 // single-GPU path runs) where RCCL is absent, and a process that already
 // loaded torch's RCCL reuses that copy instead of loading a second one.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include "nr_common.h"
 
 #include <dlfcn.h>
@@ -760,6 +764,108 @@ bool WaitFrameDelivered(RenderContext* ctx, i64 ticket) {
     NR_CHECK(hipSetDevice(ctx->device));
     return hipEventSynchronize(ctx->evDeliver[ticket]) == hipSuccess;
 }
+
+// NEW (§8e, the ingress-free assembly): this rank's bands of the frame
+// output (u8 image or YUV420P planes) copied from the GPU straight into their
+// places in a host frame -- every rank of a sharded frame delivers into the
+// same host frame (one process per GPU: a SharedHostBuffer, AllocSharedHostBuffer),
+// so the frame is assembled in host memory by each GPU's own PCIe link and no
+// GPU receives the others' bands (GatherFrameU8 + DeliverFrameU8 moves 7/8 of
+// the frame into the root over xGMI and then all of it over the root's PCIe
+// link).  Converts the owned bands first when the raster has not written them
+// (as GatherFrameU8's first half), then one strided copy per plane segment and
+// owned band slot of the pattern (3 per frame for equal shards of a YUV420P
+// frame), on the gather stream, overlapped with the next frame as
+// DeliverFrameU8.  Returns a ticket for WaitFrameDelivered, or -1.
+i64 DeliverFrameBands(RenderContext* ctx, iu8* host) {
+    NR_CHECK(hipSetDevice(ctx->device));
+    if (!host) {
+        nr_set_error_msg("DeliverFrameBands: null host frame");
+        return -1;
+    }
+    if (!frame_u8_local(ctx)) return -1;
+    const int x = ctx->frameCur;
+    iu8* const frame = ctx->frameBuf[x];
+    if (!frame) {
+        nr_set_error_msg("DeliverFrameBands: no frame output");
+        return -1;
+    }
+    ensure_comm_stream(ctx);
+    if (!ctx->evDeliver[x]) NR_CHECK(hipEventCreateWithFlags(&ctx->evDeliver[x], hipEventDisableTiming));
+    NR_CHECK(hipEventRecord(ctx->evFrameReady, ctx->stream));
+    NR_CHECK(hipStreamWaitEvent(ctx->commStream, ctx->evFrameReady, 0));
+    const FrameGeom g = frame_geom(ctx);
+    const i64 bands = (ctx->height + BAND - 1) / BAND;
+    const int P = ctx->shardPeriod;
+    const i64 full = ctx->height / BAND;   // bands [0, full) have BAND rows; band `full` (if any) is short
+    for (int sl = 0; sl < P && sl < bands; ++sl) {
+        if (ctx->shardPattern[sl] != ctx->shard) continue;
+        const i64 nb = sl < full ? (full - 1 - sl) / P + 1 : 0;   // full bands sl, sl + P, ...
+        i64 off[3], len[3], offn[3], lenn[3];
+        const int ns = band_segments(g, sl, off, len);
+        band_segments(g, sl + P, offn, lenn);
+        if (nb > 0)
+            for (int k = 0; k < ns; ++k) {
+                const size_t pitch = (size_t)(offn[k] - off[k]);   // the same segment one period on
+                NR_CHECK(hipMemcpy2DAsync(host + off[k], pitch, frame + off[k], pitch, (size_t)len[k], (size_t)nb,
+                                          hipMemcpyDeviceToHost, ctx->commStream));
+            }
+        if (full < bands && full % P == sl) {   // the frame's short last band
+            const int nl = band_segments(g, full, off, len);
+            for (int k = 0; k < nl; ++k)
+                if (len[k] > 0)
+                    NR_CHECK(hipMemcpyAsync(host + off[k], frame + off[k], (size_t)len[k], hipMemcpyDeviceToHost,
+                                            ctx->commStream));
+        }
+    }
+    NR_CHECK(hipEventRecord(ctx->evDeliver[x], ctx->commStream));
+    rotate_frame(ctx, x);   // the next frame renders into the other buffer (this one after the copies)
+    return x;
+}
+
+// NEW: pinned host memory shared between processes (POSIX shared memory
+// `name`, "/..."; every process maps and registers the same bytes): the host
+// frame the ranks' DeliverFrameBands assemble.  FreeSharedHostBuffer unmaps
+// it in this process; UnlinkSharedHostBuffer removes the name (once, by the
+// creator, after the others have mapped it or are done).
+void* AllocSharedHostBuffer(const char* name, i64 bytes) {
+    if (!name || name[0] != '/' || bytes <= 0) {
+        nr_set_error_msg("AllocSharedHostBuffer: name must start with '/' and bytes be > 0");
+        return nullptr;
+    }
+    const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) {
+        nr_set_error_msg("AllocSharedHostBuffer: shm_open failed");
+        return nullptr;
+    }
+    struct stat st;
+    if (fstat(fd, &st) != 0 || (st.st_size < bytes && ftruncate(fd, (off_t)bytes) != 0)) {
+        close(fd);
+        nr_set_error_msg("AllocSharedHostBuffer: could not size the shared memory");
+        return nullptr;
+    }
+    void* p = mmap(nullptr, (size_t)bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        nr_set_error_msg("AllocSharedHostBuffer: mmap failed");
+        return nullptr;
+    }
+    if (hipHostRegister(p, (size_t)bytes, hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        munmap(p, (size_t)bytes);
+        nr_set_error_msg("AllocSharedHostBuffer: hipHostRegister failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void FreeSharedHostBuffer(void* p, i64 bytes) {
+    if (!p) return;
+    NR_CHECK(hipHostUnregister(p));
+    munmap(p, (size_t)bytes);
+}
+
+bool UnlinkSharedHostBuffer(const char* name) { return name && shm_unlink(name) == 0; }
 
 // NEW: pinned (page-locked) host memory for DeliverFrameU8, and its release.
 void* AllocHostBuffer(i64 bytes) {

@@ -380,6 +380,21 @@ class RenderContext:
             raise RuntimeError("DeliverFrameU8 failed: " + _lib.last_error())
         return t
 
+    def deliver_frame_bands(self, dst) -> int:
+        """This rank's bands of its frame output (after its shard's frame --
+        no gather) copied straight into their places in the host frame `dst`
+        (a SharedHostBuffer every rank of the frame maps, or a HostBuffer in
+        one process), asynchronously (DeliverFrameBands); returns a ticket
+        for wait_frame_delivered().  The frame is whole once every rank's
+        copy has landed."""
+        n = int(np.prod(self.frame_output_shape()))
+        if dst.nbytes < n:
+            raise ValueError(f"deliver_frame_bands: the host buffer holds {dst.nbytes} bytes, the frame {n}")
+        t = lib.DeliverFrameBands(self._ptr, dst.ptr)
+        if t < 0:
+            raise RuntimeError("DeliverFrameBands failed: " + _lib.last_error())
+        return t
+
     def wait_frame_delivered(self, ticket: int):
         if not lib.WaitFrameDelivered(self._ptr, ticket):
             raise RuntimeError("WaitFrameDelivered failed: " + _lib.last_error())
@@ -520,6 +535,33 @@ class HostBuffer:
         if getattr(self, "ptr", None):
             lib.FreeHostBuffer(self.ptr)
             self.ptr = None
+
+
+class SharedHostBuffer:
+    """Pinned host memory shared by the processes of a sharded frame (POSIX
+    shared memory `name`, AllocSharedHostBuffer): every rank maps the same
+    host frame and delivers its bands into it (deliver_frame_bands).  The
+    creator (`owner=True`) removes the name when closed."""
+
+    def __init__(self, name: str, nbytes: int, owner: bool = False):
+        self.name, self.nbytes, self.owner = name, int(nbytes), owner
+        self.ptr = lib.AllocSharedHostBuffer(name.encode(), self.nbytes)
+        if not self.ptr:
+            raise MemoryError("AllocSharedHostBuffer failed: " + _lib.last_error())
+
+    def array(self, shape=None) -> np.ndarray:
+        a = np.ctypeslib.as_array((ctypes.c_ubyte * self.nbytes).from_address(self.ptr))
+        return a if shape is None else a[: int(np.prod(shape))].reshape(shape)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            lib.FreeSharedHostBuffer(self.ptr, self.nbytes)
+            self.ptr = None
+            if self.owner:
+                lib.UnlinkSharedHostBuffer(self.name.encode())
+
+    def __del__(self):
+        self.close()
 
 
 class PackedCommands:

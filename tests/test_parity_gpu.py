@@ -724,11 +724,13 @@ def test_hit_effect_needs_alpha_mask(gpu):
     assert not R.lib.CreateMilthmHitEffectTexture(tex._ptr, 0.1, 0.5, 1.0, 1.0, 1.0)
 
 
-def test_bench_multi_rank_orchestration_on_one_gpu(gpu, tmp_path):
+@pytest.mark.parametrize("deliver", ["none", "bands"])
+def test_bench_multi_rank_orchestration_on_one_gpu(gpu, tmp_path, deliver):
     """bench.py's N>1 path (torchrun, 2 ranks): partition calibration over
     weighted shards, barriers, max-over-ranks timing and the JSON line -- run
     with a gloo group and every rank on this one GPU (--gloo-test skips only the
-    RCCL frame gather, which needs one GPU per rank)."""
+    RCCL frame gather, which needs one GPU per rank).  deliver=bands: each rank
+    copies its bands into two shared pinned host frames (DeliverFrameBands)."""
     import json
     import socket
     import subprocess
@@ -738,13 +740,15 @@ def test_bench_multi_rank_orchestration_on_one_gpu(gpu, tmp_path):
         port = so.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(scenes.ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "5", "--warmup", "1", "--gloo-test", "--config", "c2"]
+           "--gpus", "2", "--steps", "5", "--warmup", "1", "--gloo-test", "--config", "c2", "--deliver", deliver]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 5
     assert set(d["config"]["partition_calibration_ms"]) >= {"equal", "3", "12"}
+    if deliver == "bands":
+        assert "shared pinned host frame" in d["config"]["frame_delivery"]
 
 
 @pytest.mark.parametrize("alpha", [False, True])

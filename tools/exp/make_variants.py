@@ -23,6 +23,8 @@ VARIANTS = {
     "times": ["EXP_TIMES"],
     "planr": ["EXP_PLANR"],
     "binph": ["EXP_BINPH"],
+    "warmph": ["EXP_WARMPH"],
+    "norsv": ["EXP_NORSV"],
     "sht": ["EXP_SHT"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
@@ -87,6 +89,26 @@ PATCHES = {
          "    if (tid == 0) { const u64 sh_t4 = __builtin_amdgcn_s_memrealtime();\n"
          "        atomicAdd(&g_acc[0], sh_t1 - sh_t0); atomicAdd(&g_acc[1], sh_t2 - sh_t1); atomicAdd(&g_acc[2], sh_t3 - sh_t2);\n"
          "        atomicAdd(&g_acc[5], sh_t4 - sh_t3); atomicAdd(&g_acc[3], 1ull); atomicAdd(&g_acc[4], (u64)nU); }\n}\n"),
+    ],
+    "EXP_WARMPH": [   # per-WG phase durations of k_bin_warm -> g_acc[0..3] (loads, LDS histogram, range reservation, pairs), [7] WGs; span g_exp[0..1]
+        ("    if (tid == 0) wgPairs = 0;\n",
+         "    if (tid == 0) wgPairs = 0;\n    const u64 w_t0 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("    __syncthreads();   // (hist and wgPairs zeroed)\n",
+         "    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();   // (hist and wgPairs zeroed)\n    const u64 w_t1 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("    if (LDSH) {\n        __syncthreads();\n        for (int b = tid; b < hbins; b += 256) {   // reserve each touched tile's range once\n",
+         "    __syncthreads();\n    const u64 w_t2 = __builtin_amdgcn_s_memrealtime();\n    if (LDSH) {\n        for (int b = tid; b < hbins; b += 256) {   // reserve each touched tile's range once\n"),
+        ("    __syncthreads();   // (LDS ranges reserved; wgPairs complete)\n",
+         "    __syncthreads();   // (LDS ranges reserved; wgPairs complete)\n    const u64 w_t3 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("                if (slot < end) list[slot] = (u32)t;\n            }\n        }\n    }\n}\n",
+         "                if (slot < end) list[slot] = (u32)t;\n            }\n        }\n    }\n"
+         "    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();\n"
+         "    if (tid == 0) { const u64 w_t4 = __builtin_amdgcn_s_memrealtime();\n"
+         "        atomicAdd(&g_acc[0], w_t1 - w_t0); atomicAdd(&g_acc[1], w_t2 - w_t1); atomicAdd(&g_acc[2], w_t3 - w_t2);\n"
+         "        atomicAdd(&g_acc[3], w_t4 - w_t3); atomicAdd(&g_acc[7], 1ull); atomicMin(&g_exp[0], w_t0); atomicMax(&g_exp[1], w_t4); }\n}\n"),
+    ],
+    "EXP_NORSV": [   # timing only (wrong lists): k_bin_warm's range reservation without its global atomics
+        ("                const u32 start = beg + atomicAdd(&cur[tile], h) - epoch * (end - beg);\n",
+         "                const u32 start = EXP_NORSV ? beg : beg + atomicAdd(&cur[tile], h) - epoch * (end - beg);\n"),
     ],
     "EXP_NOROWS": [
         ("            if (r0 < r1 && !big) {\n",
