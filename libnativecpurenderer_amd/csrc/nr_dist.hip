@@ -777,6 +777,38 @@ bool WaitFrameDelivered(RenderContext* ctx, i64 ticket) {
 // owned band slot of the pattern (3 per frame for equal shards of a YUV420P
 // frame), on the gather stream, overlapped with the next frame as
 // DeliverFrameU8.  Returns a ticket for WaitFrameDelivered, or -1.
+// Band delivery copies: a rank owning at most BAND_KERNEL_MAX bytes of the frame
+// output writes them with one kernel of BAND_WG workgroups into the host frame's
+// device address; larger shares take one strided runtime copy per plane segment
+// and owned slot of the pattern.  Measured with the copies beside the next frame
+// (C3 YUV420P, bench.py --deliver bands, profiles/r05/ab_band_copy.txt): an 8-way
+// share (1.55 MB) 0.0804 -> 0.0723 ms with the kernel (32 workgroups: 0.0733);
+// a 2-way share (6.2 MB) 0.1617 with the strided copies against 0.1727.
+constexpr i64 BAND_KERNEL_MAX = 3 << 20;
+constexpr int BAND_WG = 8;
+}  // extern "C"
+namespace {
+// This rank's bands of `frame` to the same offsets of the host frame (its
+// device address): BAND_WG workgroups stride over every owned segment.
+template <typename V>
+__global__ __launch_bounds__(256) void k_bands_to_host(const iu8* __restrict__ frame, iu8* __restrict__ host,
+                                                       FrameGeom g, ShardMap sm, int sel, i64 bands) {
+    for (i64 b = 0; b < bands; ++b) {
+        if (sm.pattern[b % sm.period] != sel) continue;
+        i64 off[3], len[3];
+        const int ns = band_segments(g, b, off, len);
+        for (int k = 0; k < ns; ++k) {
+            const V* src = reinterpret_cast<const V*>(frame + off[k]);
+            V* dst = reinterpret_cast<V*>(host + off[k]);
+            const i64 n = len[k] / (i64)sizeof(V);
+            for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (i64)gridDim.x * blockDim.x)
+                dst[i] = src[i];
+        }
+    }
+}
+}  // namespace
+extern "C" {
+
 i64 DeliverFrameBands(RenderContext* ctx, iu8* host) {
     NR_CHECK(hipSetDevice(ctx->device));
     if (!host) {
@@ -798,7 +830,25 @@ i64 DeliverFrameBands(RenderContext* ctx, iu8* host) {
     const i64 bands = (ctx->height + BAND - 1) / BAND;
     const int P = ctx->shardPeriod;
     const i64 full = ctx->height / BAND;   // bands [0, full) have BAND rows; band `full` (if any) is short
-    for (int sl = 0; sl < P && sl < bands; ++sl) {
+    const bool viaKernel = owned_bytes(ctx, ctx->shard) <= BAND_KERNEL_MAX;
+    if (viaKernel) {
+        void* hdev = nullptr;
+        NR_CHECK(hipHostGetDevicePointer(&hdev, host, 0));
+        bool vec = (reinterpret_cast<uintptr_t>(hdev) | reinterpret_cast<uintptr_t>(frame)) % 16 == 0;
+        for (i64 b = 0; b < bands && vec; ++b) {
+            i64 off[3], len[3];
+            const int ns = band_segments(g, b, off, len);
+            for (int k = 0; k < ns; ++k) vec = vec && off[k] % 16 == 0 && len[k] % 16 == 0;
+        }
+        if (vec)
+            hipLaunchKernelGGL(k_bands_to_host<uint4>, dim3(BAND_WG), dim3(256), 0, ctx->commStream, frame,
+                               (iu8*)hdev, g, shard_map(ctx), ctx->shard, bands);
+        else
+            hipLaunchKernelGGL(k_bands_to_host<iu8>, dim3(BAND_WG), dim3(256), 0, ctx->commStream, frame,
+                               (iu8*)hdev, g, shard_map(ctx), ctx->shard, bands);
+        NR_CHECK(hipGetLastError());
+    }
+    for (int sl = 0; sl < P && sl < bands && !viaKernel; ++sl) {
         if (ctx->shardPattern[sl] != ctx->shard) continue;
         const i64 nb = sl < full ? (full - 1 - sl) / P + 1 : 0;   // full bands sl, sl + P, ...
         i64 off[3], len[3], offn[3], lenn[3];
