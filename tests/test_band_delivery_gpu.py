@@ -31,7 +31,8 @@ def _reference(R, W, H, fmt, k):
 
 @pytest.mark.parametrize("fmt", ["rgb", "yuv420p"])
 @pytest.mark.parametrize("W,H,part", [(320, 256, ("equal", 2)), (330, 330, ("equal", 3)),
-                                      (256, 270, ("slots", [3, 1, 2])), (200, 100, ("equal", 1))])
+                                      (256, 270, ("slots", [3, 1, 2])), (200, 100, ("equal", 1)),
+                                      (2048, 2016, ("equal", 2))])   # (> 3 MB per rank: the strided copies)
 def test_bands_assemble_the_frame(fmt, W, H, part):
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     xy, z, c = band_rank.mesh(W, H)
