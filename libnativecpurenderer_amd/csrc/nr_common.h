@@ -345,18 +345,11 @@ __device__ __forceinline__ u32 nr_quantize_depth_bl(f64 z) {
 // fragment.  (In C++ an out-of-range cast is undefined, hence the asm.)
 // Pinned against nr_quantize_depth on NaN, infinities, huge and boundary
 // values by tests/test_depth_edges_gpu.py.
-#ifndef NR_QUANT_HW
-#define NR_QUANT_HW 1
-#endif
 __device__ __forceinline__ u32 nr_quantize_depth_hw(f64 z) {
-#if NR_QUANT_HW
     const f64 p = z * 4294967295.0;
     u32 r;
     asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(p));
     return r;
-#else
-    return nr_quantize_depth_bl(z);
-#endif
 }
 
 // Bytes of the context's frame output (frameFormat: u8 image or YUV420P).

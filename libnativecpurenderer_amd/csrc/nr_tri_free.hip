@@ -70,11 +70,6 @@ __device__ __forceinline__ void probe_item(u32 item, uint4 d, u64 t0, u64 t1, in
 #define NR_PROBE_STAMP(k) do { } while (0)
 #endif
 
-// Fast clear (RenderContext::tileStamp): 0 = empty tiles write their pending
-// clears in k_vis (A/B).
-#ifndef NR_FAST_CLEAR
-#define NR_FAST_CLEAR 1
-#endif
 
 constexpr int VWG = 256;  // k_vis workgroup
 // k_vis occupancy: 4 waves per SIMD (<= 128 VGPRs, and LDS <= 40 KB per
@@ -2200,7 +2195,7 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         const size_t n = (size_t)nr_frame_bytes(ctx);
         if (n <= ctx->frameU8cap) fp.frameU8 = ctx->frameU8;
     }
-    if (!ordered && (fp.pendColor || fp.pendDepth) && NR_FAST_CLEAR)   // (k_vis: empty tiles' clears stay pending)
+    if (!ordered && (fp.pendColor || fp.pendDepth))   // fast clear: the empty tiles' clears stay pending (k_vis)
         fp.tileStamp = tile_stamps(ctx, (i64)fp.tiles_x * fp.tiles_y), fp.tileEpoch = ctx->tileEpoch;
     BinParams bp;
     bp.src = src;
