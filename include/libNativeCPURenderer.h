@@ -230,7 +230,8 @@ i64 GetDeviceCount(void);
 i64 GetContextDevice(RenderContext* ctx);
 void Flush(RenderContext* ctx);                  /* wait for every queued draw */
 void ResolvePending(RenderContext* ctx);         /* materialise deferred clears */
-void* GetDeviceBufferPtr(RenderContext* ctx);    /* framebuffer in HBM (RCCL / interop) */
+void* GetDeviceBufferPtr(RenderContext* ctx);    /* framebuffer in HBM (RCCL / interop); writes the pending
+                                                    clears first -- the bytes are current after Flush */
 void* GetStreamPtr(RenderContext* ctx);          /* hipStream_t the context launches on */
 void GetBufferAsUInt8Device(RenderContext* ctx, iu8* dev_out); /* cpp:52-57 into HBM */
 void GetTextureBuffer(Texture* tex, f64* out);

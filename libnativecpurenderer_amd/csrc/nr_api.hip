@@ -758,7 +758,14 @@ void ResolvePending(RenderContext* ctx) {
 }
 
 // Raw device pointers / stream, for RCCL or torch interop (no torch types).
-void* GetDeviceBufferPtr(RenderContext* ctx) { return ctx->buffer; }
+// (the pending clears -- whole-frame and per-tile, the fast clear -- are
+// written first, so the bytes behind the pointer are the framebuffer's value
+// once the stream has drained: Flush)
+void* GetDeviceBufferPtr(RenderContext* ctx) {
+    NR_CHECK(hipSetDevice(ctx->device));
+    nr_materialize(ctx);
+    return ctx->buffer;
+}
 void* GetStreamPtr(RenderContext* ctx) { return (void*)ctx->stream; }
 
 // Switching off does not synchronise: recorded pairs are read at the next

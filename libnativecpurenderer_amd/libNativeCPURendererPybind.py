@@ -296,6 +296,8 @@ class RenderContext:
         return lib.GetContextDevice(self._ptr)
 
     def device_buffer_ptr(self) -> int:
+        """Device address of the f64 framebuffer (GetDeviceBufferPtr: the pending
+        clears are written first; the bytes are current once flush() returns)."""
         return lib.GetDeviceBufferPtr(self._ptr)
 
     def stream_ptr(self) -> int:
