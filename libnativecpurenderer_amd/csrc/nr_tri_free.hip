@@ -328,117 +328,6 @@ __global__ __launch_bounds__(PLAN_T) void k_free_plan(u32* __restrict__ cnt, int
     }
 }
 
-// The same plan with one 256-thread workgroup (4 waves, <= 128 VGPRs, < 1 KB
-// LDS): it fits the slot a finishing k_vis workgroup frees, so it runs while
-// the previous batch's k_vis holds the chip (the 1024-thread plan needs a
-// whole CU and waits for k_vis to drain).  Each thread owns PS consecutive
-// tiles of a block of 256 * PS (thread-serial scan, then one workgroup scan).
-constexpr int PS_T = 256, PS_W = PS_T / 64, PS = 16;
-__global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int ntiles, int tiles_x, int period,
-                                                      u64 mask, u32* __restrict__ off, uint4* __restrict__ items,
-                                                      u32* __restrict__ cur, u32* __restrict__ totals,
-                                                      u64* __restrict__ host_totals, u32 cap, u32 icap, u32 seq,
-                                                      u32 slice_target, u32 kcap, u32 split_at, u32 dslice) {
-    __shared__ u32 sh[3][PS_W];
-    __shared__ u32 bcnt[PLAN_NB], bcur[PLAN_NB];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid < PLAN_NB) bcnt[tid] = 0;
-    // pass 0: pair total (slice length) and dense-tile count
-    u32 a = 0, hv = 0;
-    for (int b0 = 0; b0 < ntiles; b0 += PS_T * PS) {
-        const int i0 = b0 + tid * PS;
-        u32 c[PS];
-#pragma unroll
-        for (int j = 0; j < PS; ++j) c[j] = i0 + j < ntiles ? cnt[i0 + j] : 0u;
-#pragma unroll
-        for (int j = 0; j < PS; ++j) {
-            a += c[j];
-            hv += c[j] >= HEAVY_PAIRS ? 1u : 0u;
-        }
-    }
-    a = wave_scan(a, lane); hv = wave_scan(hv, lane);
-    if (lane == 63) { sh[0][w] = a; sh[1][w] = hv; }
-    __syncthreads();
-    u32 ta = 0, th = 0;
-#pragma unroll
-    for (int k = 0; k < PS_W; ++k) { ta += sh[0][k]; th += sh[1][k]; }
-    u32 slice = SLICE_MIN;
-    while (slice < SLICE && (u64)slice * slice_target < ta) slice <<= 1;
-    u32 lim, dsl;
-    split_limits(slice, split_at, dslice, lim, dsl);
-    __syncthreads();
-    // pass 1: item totals and items per size class
-    u32 b = 0, m = 0;
-    for (int b0 = 0; b0 < ntiles; b0 += PS_T * PS) {
-        const int i0 = b0 + tid * PS;
-        u32 c[PS];
-#pragma unroll
-        for (int j = 0; j < PS; ++j) c[j] = i0 + j < ntiles ? cnt[i0 + j] : 0u;
-#pragma unroll
-        for (int j = 0; j < PS; ++j) {
-            if (i0 + j >= ntiles) break;
-            const u32 ni = tile_items(c[j], owned_row((i0 + j) / tiles_x, period, mask), lim, dsl);
-            b += ni;
-            m += ni > 1 ? ni : 0u;
-            if (ni) atomicAdd(&bcnt[size_class(c[j], lim, dsl)], ni);
-        }
-    }
-    b = wave_scan(b, lane); m = wave_scan(m, lane);
-    if (lane == 63) { sh[1][w] = b; sh[2][w] = m; }
-    __syncthreads();
-    u32 tb = 0, tm = 0;
-#pragma unroll
-    for (int k = 0; k < PS_W; ++k) { tb += sh[1][k]; tm += sh[2][k]; }
-    const bool fits = ta <= cap && tb <= icap && tm <= kcap;
-    if (tid == 0) {
-        u32 base = 0;
-        for (int k = PLAN_NB - 1; k >= 0; --k) { bcur[k] = base; base += bcnt[k]; }
-    }
-    __syncthreads();
-    // pass 2: offsets and items
-    u32 carry = 0;
-    for (int b0 = 0; b0 < ntiles; b0 += PS_T * PS) {
-        const int i0 = b0 + tid * PS;
-        u32 c[PS];
-#pragma unroll
-        for (int j = 0; j < PS; ++j) c[j] = i0 + j < ntiles ? cnt[i0 + j] : 0u;
-        u32 loc = 0;
-#pragma unroll
-        for (int j = 0; j < PS; ++j) loc += c[j];
-        const u32 inc = wave_scan(loc, lane);
-        if (lane == 63) sh[0][w] = inc;
-        __syncthreads();
-        u32 ea = carry + inc - loc;
-#pragma unroll
-        for (int k = 0; k < PS_W; ++k) {
-            if (k < w) ea += sh[0][k];
-            carry += sh[0][k];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < PS; ++j) {
-            const int i = i0 + j;
-            if (i >= ntiles) break;
-            off[i] = ea;
-            const u32 ni = tile_items(c[j], owned_row(i / tiles_x, period, mask), lim, dsl);
-            if (fits && ni) {
-                const u32 eb = atomicAdd(&bcur[size_class(c[j], lim, dsl)], ni);
-                for (u32 k = 0; k < ni; ++k) items[eb + k] = tile_item((u32)i, ea, c[j], k, ni);
-            }
-            cnt[i] = 0;
-            cur[i] = 0;
-            ea += c[j];
-        }
-    }
-    if (tid == 0) {
-        off[ntiles] = ta;
-        const u32 t[7] = {ta, tb, tm, fits ? 1u : 0u, seq, th, 0u};
-        for (int k = 0; k < 4; ++k) totals[k] = t[k];
-        for (int k = 0; k < 7; ++k)   // (host copy: see k_free_plan)
-            __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
 // The same plan with every tile count read once, into registers: thread t
 // owns PR = 4 * ceil(ntiles / 4T) <= 16 consecutive tiles [t*PR, t*PR + PR), read and
 // written as 16-byte vectors (the tile arrays are allocated to TILE_ARR entries,
@@ -448,8 +337,7 @@ __global__ __launch_bounds__(PS_T) void k_free_plan_s(u32* __restrict__ cnt, int
 // atomics (a wave's lanes mostly share a class, and such atomics serialise):
 // per-lane class counts in registers, per-class wave scans, one LDS slot per
 // (class, wave).  Launched with T = PLAN_T = 1024 threads whenever ntiles <=
-// 16 * T (16384 tiles, an 8K frame) and the batch does not run beside a long
-// raster (free_enqueue).
+// 16 * T (16384 tiles, an 8K frame; free_enqueue).
 constexpr int PR_MAX = 16;
 constexpr int TILE_ARR = 16 * 1024 + 4;   // minimum length of the per-tile arrays
 template <int T, int PR>
@@ -585,18 +473,6 @@ __global__ __launch_bounds__(T) void k_free_plan_r(u32* __restrict__ cnt, int nt
         for (int k = 0; k < 7; ++k)   // (host copy: see k_free_plan)
             __hip_atomic_store(&host_totals[k], ((u64)seq << 32) | t[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-}
-
-// Which plan kernel: the 256-thread one when the batch's owned share is large
-// (>= 2^17 triangles' worth: C3 unsharded 0.167 -> 0.160 ms per frame, C3 4-way
-// share 0.0654 -> 0.0627 ms; the plan runs beside the previous, long k_vis),
-// the 1024-thread one otherwise: a short k_vis leaves the plan mostly alone and
-// the wider workgroup is faster (C3 8-way share 0.0535 -> 0.0516 ms; C2, 10k
-// triangles, 0.0802 -> 0.069 ms).
-static bool owned_share_large(int period, u64 mask, i64 ntri) {
-    const u64 m = period >= 64 ? mask : (mask & ((1ull << period) - 1ull));
-    const f64 share = period == 1 ? 1.0 : (f64)__builtin_popcountll(m) / (f64)period;
-    return (f64)ntri * share >= (f64)(1 << 17);
 }
 
 template <bool LDSH>
@@ -1751,25 +1627,24 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         const u32 seq = ++sc.planSeq;
         *seqOut = seq;
         nr_timing_begin_on(ctx, NRK_TRI_SCAN, &e0, &e1, sb);
-        // a large owned share (a long k_vis of the previous batch to run beside)
-        // takes the narrow plan kernel; an idle GPU the faster wide one
-        const bool besideRaster = !idle && owned_share_large(fp.period, fp.mask, src.n);
         const u32 icap32 = (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull);
         // (an ordered batch uses no key slots, and its lists must fit the raster's LDS sort)
         const u32 kcap32 = ordered ? 0xFFFFFFFFu : (u32)std::min<size_t>(sc.kslot_cap / (TH * TW), 0xFFFFFFF0ull);
         const u32 maxc = ordered ? ORD_SORT_CAP : 0u;
         const u32 sat = sc.splitAt ? sc.splitAt : SPLIT_AT, dsl = sc.dslice ? sc.dslice : DSLICE;
-        if ((!besideRaster && ntiles <= PLAN_T * PR_MAX) || ordered) {   // (ordered: ntiles <= ORD_BIN_TILES)
+        if (ntiles <= PLAN_T * PR_MAX || ordered) {   // (ordered: ntiles <= ORD_BIN_TILES)
             // the register plan: one 1024-thread workgroup, PR = tiles per
             // thread -> 4, 8 or 16 (PR 4: 107 VGPRs; PR 8 and 16 spill a few,
             // 4 and 39, at __launch_bounds__(1024)'s 128).  It needs a whole CU
             // (an ordered batch's plan beside the ordered raster therefore waits
             // for the raster's tail, which measured better than a 512-thread
             // instance that runs the chain earlier, beside it: C5 +10 %,
-            // profiles/r03_c5/ab_plan512.txt), so beside a long raster
-            // (besideRaster) the 256-thread, 65-VGPR multi-round k_free_plan_s
-            // runs instead: it fits the slot a finishing k_vis workgroup frees
-            // (C3 0.163 vs 0.172 ms; profiles/r02_c3/ab_plan_r.txt)
+            // profiles/r03_c5/ab_plan512.txt).  A 256-thread multi-round plan
+            // that fits beside a running k_vis was kept for large batches until
+            // round 5 (C3 0.163 vs 0.172 ms then, profiles/r02_c3/ab_plan_r.txt);
+            // with the faster raster the chain's count ends with the raster and
+            // the wide plan is faster: a cold C3 frame (c3_animated) 0.157 ->
+            // 0.150 ms (profiles/r05/ab_plan_wide.txt).
             const int per = (ntiles + PLAN_T - 1) / PLAN_T;
 #define NR_PLAN_R(PP) hipLaunchKernelGGL((k_free_plan_r<PLAN_T, PP>), dim3(1), dim3(PLAN_T), 0, sb, F.fcnt, ntiles, \
                                          fp.tiles_x, fp.period, fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, \
@@ -1777,10 +1652,6 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
             if (per <= 4) NR_PLAN_R(4); else if (per <= 8) NR_PLAN_R(8); else NR_PLAN_R(16);
 #undef NR_PLAN_R
         }
-        else if (besideRaster)
-            hipLaunchKernelGGL(k_free_plan_s, dim3(1), dim3(PS_T), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
-                               fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
-                               (u32)std::min<size_t>(F.fitems_cap, 0xFFFFFFF0ull), seq, SLICE_TARGET, kcap32, sat, dsl);
         else
             hipLaunchKernelGGL(k_free_plan, dim3(1), dim3(1024), 0, sb, F.fcnt, ntiles, fp.tiles_x, fp.period,
                                fp.mask, F.foff, F.fitems, F.fcur, F.dplan, F.d_hplan, (u32)cap,
