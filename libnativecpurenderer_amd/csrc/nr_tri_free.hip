@@ -1995,7 +1995,11 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (gated && !F.gate) {
         NR_CHECK(hipMalloc(&F.gate, 4 * sizeof(u32)));
         NR_CHECK(hipMalloc(&F.gplan, 4 * sizeof(u32)));
-        NR_CHECK(hipMemset(F.gate, 0, 4 * sizeof(u32)));
+        // zeroed in order on the signalling stream: a plain hipMemset (null
+        // stream) may still be pending when the first signal lands and zero
+        // it -- that raster's wait then times out (seen with a cold-batch gate
+        // on a busy device, profiles/r05/ab_cold_gate.txt)
+        NR_CHECK(hipMemsetAsync(F.gate, 0, 4 * sizeof(u32), sb));
         F.gateTok = 0;
     }
     const bool xs = sb != sa && !e1 && !gated;
