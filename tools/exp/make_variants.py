@@ -26,9 +26,14 @@ VARIANTS = {
     "warmph": ["EXP_WARMPH"],
     "norsv": ["EXP_NORSV"],
     "sht": ["EXP_SHT"],
+    "nosum": ["EXP_NOSUM"],
 }
 # define -> [(anchor, replacement)]; only the patches of the defines in use are applied
 PATCHES = {
+    "EXP_NOSUM": [   # no pair-sum atomic in k_bin_warm (and no sum check in k_vis): its cost
+        ("    if (tid == 0 && wgPairs) atomicAdd(&wstat[WS_SUM], wgPairs);\n", "\n"),
+        ("        fb = !plan[3] || wt == wc.tag || ws != wc.expect;\n", "        fb = !plan[3] || wt == wc.tag;\n"),
+    ],
     "EXP_BINPH": [   # per-WG phase durations of k_free_count / k_free_emit -> g_acc[0..3] (count), g_acc[4..6] (emit), spans g_exp
         ("    f64 pxy[TPT][6];\n#pragma unroll\n    for (int k = 0; k < TPT; ++k) {\n        const i64 t = base + k * 256 + tid;\n        if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);\n    }\n",
          "    const u64 c_t0 = __builtin_amdgcn_s_memrealtime();\n    f64 pxy[TPT][6];\n#pragma unroll\n    for (int k = 0; k < TPT; ++k) {\n        const i64 t = base + k * 256 + tid;\n        if (t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);\n    }\n"
