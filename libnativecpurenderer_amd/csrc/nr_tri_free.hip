@@ -552,8 +552,8 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 // takes slots from there (cursor - epoch * count, count = off[t + 1] - off[t]).
 // Checks (wstat, beside the cursors): a tile found over its range stores the
 // batch's tag in wstat[WS_TAG] (its excess pairs are dropped), and every
-// workgroup adds its pair total to its lane of the pair sum (wstat[WS_SUM..],
-// zeroed with the cursors), whose lanes' total after the e-th warm batch must equal
+// workgroup adds its pair total to wstat[WS_SUM] (zeroed with the cursors),
+// which after the e-th warm batch must equal
 // (e + 1) * the schedule's pairs -- so an undercount anywhere is seen too.
 // k_vis reads both before it trusts the lists (WarmCheck).  `inject` (tests
 // only, SetWarmFaultInjection): 1 shifts the epoch (every touched tile out of
@@ -587,12 +587,7 @@ __device__ __forceinline__ bool cluster_may_touch(const BinParams& bp, const f64
     return ty1 >= ty0 + 64;
 }
 
-// The warm checks' words, right after a set's ntiles cursors: the error tag,
-// then the pair sum spread over WS_LANES words a cache line apart (workgroup
-// b adds to lane b % WS_LANES): one shared word took the ~4000 workgroups'
-// atomics one at a time, 3 us of a 1080p frame's 18 us binning
-// (profiles/r05/ab_pair_sum.txt); k_vis sums the lanes with one wave load.
-enum { WS_TAG = 0, WS_SUM = 32, WS_LANES = 64, WS_STRIDE = 32, WS_WORDS = WS_SUM + WS_LANES * WS_STRIDE };
+enum { WS_SUM = 0, WS_TAG = 1 };   // the warm checks' words, right after a set's ntiles cursors
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32* __restrict__ off,
                                                   u32* __restrict__ cur, u32* __restrict__ list,
@@ -676,7 +671,7 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
         }
     }
     __syncthreads();   // (LDS ranges reserved; wgPairs complete)
-    if (tid == 0 && wgPairs) atomicAdd(&wstat[WS_SUM + (blockIdx.x % WS_LANES) * WS_STRIDE], wgPairs);
+    if (tid == 0 && wgPairs) atomicAdd(&wstat[WS_SUM], wgPairs);
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
@@ -1013,28 +1008,7 @@ struct WarmCheck {
     const u32* wstat;
     u32 tag, expect;
     u32* hfail;
-    u32 pre;   // 1: k_gate_wait ran the checks; the plan's fits word says 1 (trusted) or 4 (fall back)
 };
-
-// The warm checks of one batch, by one whole wave (each lane reads one pair-sum
-// word); `report`: the lane that writes the reason to *hfail on a failure.
-__device__ __forceinline__ bool warm_check(const WarmCheck& wc, bool fits, bool report) {
-    const u32 wt = __hip_atomic_load(&wc.wstat[WS_TAG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    static_assert(WS_LANES == 64, "one lane per pair-sum word");
-    u32 ws = __hip_atomic_load(&wc.wstat[WS_SUM + (threadIdx.x & 63) * WS_STRIDE], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int o = 32; o; o >>= 1) ws += __shfl_xor(ws, o);   // (every wave: the same sum, no barrier)
-    const bool fb = !fits || wt == wc.tag || ws != wc.expect;
-    if (fb && report) {   // (the words read, for the message; then the reason)
-        __hip_atomic_store(&wc.hfail[1], ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&wc.hfail[2], wc.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&wc.hfail[3], (wt == wc.tag ? 1u : 0u) | (fits ? 0u : 2u), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&wc.hfail[0], fits ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    return fb;
-}
 
 template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
@@ -1057,10 +1031,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
     __shared__ int sLast;
     __shared__ unsigned long long sFrag;
     bool fb = false;   // fallback: every triangle of the batch against every tile (WarmCheck)
-    if (wc.pre) {
-        fb = plan[3] != 1;   // (checked and reported by k_gate_wait)
-    } else if (wc.wstat) {
-        fb = warm_check(wc, plan[3] != 0, blockIdx.x == 0 && threadIdx.x == 0);
+    if (wc.wstat) {
+        const u32 wt = __hip_atomic_load(&wc.wstat[WS_TAG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u32 ws = __hip_atomic_load(&wc.wstat[WS_SUM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fb = !plan[3] || wt == wc.tag || ws != wc.expect;
+        if (fb && blockIdx.x == 0 && threadIdx.x == 0) {   // (the words read, for the message; then the reason)
+            __hip_atomic_store(&wc.hfail[1], ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&wc.hfail[2], wc.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&wc.hfail[3], (wt == wc.tag ? 1u : 0u) | (plan[3] ? 0u : 2u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&wc.hfail[0], plan[3] ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     } else if (!plan[3]) {
         return;
     }
@@ -1870,29 +1851,19 @@ static void warm_poll(RenderContext* ctx) {
 __global__ void k_gate_signal(u32* __restrict__ gate, u32 tok) {
     if (threadIdx.x == 0) __hip_atomic_store(gate, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// With the batch's checks (wc.wstat), the one wave also runs them once here --
-// off the raster's workgroups -- and hands k_vis the verdict (fits word 1
-// trusted, 4 fall back; WarmCheck.pre).
 __global__ void k_gate_wait(const u32* __restrict__ gate, u32 tok, const u32* __restrict__ splan,
-                            u32* __restrict__ gplan, const WarmCheck wc) {
-    __shared__ u32 sOk;
-    if (threadIdx.x == 0) {
-        const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-        u32 ok = 1;
-        while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
-                ok = 0;
-                break;
-            }
+                            u32* __restrict__ gplan) {
+    if (threadIdx.x != 0) return;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    bool ok = true;
+    while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+            ok = false;
+            break;
         }
-        sOk = ok;
     }
-    __syncthreads();
-    const bool ok = sOk != 0;
-    u32 fits = ok ? splan[3] : 0u;   // {pairs, items, slices, fits}
-    if (wc.wstat) fits = warm_check(wc, fits != 0, threadIdx.x == 0) ? 4u : 1u;
-    if (threadIdx.x < 4) gplan[threadIdx.x] = threadIdx.x == 3 ? fits : splan[threadIdx.x];
+    for (int k = 0; k < 4; ++k) gplan[k] = (k == 3 && !ok) ? 0u : splan[k];   // {pairs, items, slices, fits}
 }
 
 // The binning blocks (256 * TPT triangles) of a schedule with a cluster that
@@ -1978,7 +1949,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         NR_CHECK(hipHostGetDevicePointer((void**)&sc.dfail, sc.hfail, 0));
     }
     // cursors [0, ntiles), then the batch checks {error tag, pair sum} (WarmCheck)
-    const size_t tneed = std::max<size_t>((size_t)ntiles + WS_WORDS, TILE_ARR);
+    const size_t tneed = std::max<size_t>((size_t)ntiles + 2, TILE_ARR);
     const bool grow = F.ftile_cap < tneed || !F.fcnt || F.flist_cap < std::max<size_t>(S.pairs, 1) ||
                       sc.kslot_cap < std::max<size_t>(S.split, 1) * (TH * TW) || sc.fdone_cap < (size_t)ntiles + 1;
     if (grow) {   // (first use of a set, or a larger schedule: rare)
@@ -2011,7 +1982,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     // cursors: epoch e of this schedule on this set (k_bin_warm); zeroed for a
     // new schedule, after a cold batch on the set, or before they could wrap
     if (F.curGen != S.gen || (u64)(F.curEpoch + 1) * std::max<u32>(S.pairs, 1) >= 0xF0000000ull) {
-        NR_CHECK(hipMemsetAsync(F.fcur, 0, ((size_t)ntiles + WS_WORDS) * sizeof(u32), sb));   // (and the checks)
+        NR_CHECK(hipMemsetAsync(F.fcur, 0, ((size_t)ntiles + 1) * sizeof(u32), sb));   // (and the pair sum)
         F.curGen = S.gen;
         F.curEpoch = 0;
     }
@@ -2036,7 +2007,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const u32 epoch = F.curEpoch++;
     if (++sc.warmTag == 0) sc.warmTag = 1;
     const u32 tag = sc.warmTag;
-    u32* const wstat = F.fcur + ntiles;   // {error tag, pair-sum lanes} (WS_TAG, WS_SUM)
+    u32* const wstat = F.fcur + ntiles;   // {pair sum, error tag} (WS_SUM, WS_TAG)
     const int inject = sc.warmInject;
     sc.warmInject = 0;
     // cluster culling of the rank's tile rows, and only the schedule's active blocks launched
@@ -2063,7 +2034,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         if (inject != 2)   // (2: the token is withheld -- tests of the timeout)
             hipLaunchKernelGGL(k_gate_signal, dim3(1), dim3(64), 0, sb, F.gate, F.gateTok);
         hipLaunchKernelGGL(k_gate_wait, dim3(1), dim3(64), 0, sa, (const u32*)F.gate, F.gateTok, (const u32*)S.dplan,
-                           F.gplan, WarmCheck{wstat, tag, (epoch + 1) * S.pairs, sc.dfail, 0u});
+                           F.gplan);
         NR_CHECK(hipGetLastError());
         visPlan = F.gplan;
     } else if (sb != sa) {
@@ -2077,7 +2048,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (S.nitems > 0) {
         nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = !e1;
-        const WarmCheck wc{wstat, tag, (epoch + 1) * S.pairs, sc.dfail, gated ? 1u : 0u};
+        const WarmCheck wc{wstat, tag, (epoch + 1) * S.pairs, sc.dfail};
         launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa,
                        vs ? F.evVis : nullptr, zmode, fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
