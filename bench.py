@@ -102,8 +102,7 @@ def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True, frame_out="rgb"):
 # --warmup 5 --steps 20) would otherwise time part of the ramp (~3-6 %,
 # profiles/r04/warmup_steps20.txt).  Reported as "clock_settle" in the line.
 CLOCK_SETTLE_MS = 60.0
-EVENT_EVERY = 10   # timed-region frames per HIP-event-timed frame of the dominant kernel (each record pair
-                   # perturbs the stream: 1 in 4 cost ~7 % of C3 throughput, 1 in 10 ~2 %)
+EVENT_EVERY = 1    # timed-region frames per timed launch of the dominant kernel (--event-every)
 
 KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)"}
 
@@ -146,6 +145,44 @@ def load_pmc_traffic(cfg_name, nsh=1, slots=None, frame_out="rgb", kernel=None):
         if d.get("config") == tag and (kernel is None or d.get("kernel", "").startswith(kernel)):
             return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
     return None, None
+
+
+VERIFY_KEYS = ("verified", "warm_failures", "verify_digest", "verified_bands", "verified_buffers",
+               "verify_mismatches", "verify_note", "fragments_match_oracle")
+DIGEST_FILE = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
+BAND_ROWS = 32   # digest unit: one tile row (the tile-row shards' unit)
+
+
+def band_digest(kind, a, W, H, b):
+    """sha256[:32] of band b (rows [32b, 32b+32)) of one frame buffer: f64 / depth /
+    u8 RGB rows, or for "yuv420p" the band's Y rows, then its U rows, then its V
+    rows of the flat planes (tests/golden/make_bench_digests.py writes the oracle's)."""
+    import hashlib
+    r0, r1 = b * BAND_ROWS, min(H, (b + 1) * BAND_ROWS)
+    if kind == "yuv420p":
+        cw, ch = W // 2, H // 2
+        a = np.asarray(a).reshape(-1)
+        y = a[:W * H].reshape(H, W)
+        u = a[W * H:W * H + cw * ch].reshape(ch, cw)
+        v = a[W * H + cw * ch:W * H + 2 * cw * ch].reshape(ch, cw)
+        data = y[r0:r1].tobytes() + u[r0 // 2:r1 // 2].tobytes() + v[r0 // 2:r1 // 2].tobytes()
+    else:
+        data = np.ascontiguousarray(a[r0:r1]).tobytes()
+    return hashlib.sha256(data).hexdigest()[:32]
+
+
+def digest_key(cfg_name, cfg, frame_index):
+    """Entry of bench_digests.json for the frame with this index (c3_animated
+    alternates its transform with the frame index's parity)."""
+    return cfg_name + (f"@{frame_index % 2}" if cfg.get("animate") else "")
+
+
+def load_digests():
+    try:
+        with open(DIGEST_FILE) as f:
+            return json.load(f)
+    except OSError:
+        return {}
 
 
 def host_cpu():
@@ -293,6 +330,54 @@ class Runner:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def verify(self, last_i):
+        """After the timed region: the last timed frame read back and checked,
+        band by band, against the oracle's digests of the same frame
+        (tests/golden/bench_digests.json) -- the f64 framebuffer and u32 depth
+        of this rank's owned bands, the frame output on the device (every band
+        on the gathering root, the owned ones elsewhere) and, when the frame is
+        delivered to host memory, the host frame of the last step.  Also the
+        warm binning's failure count (a failed warm batch falls back to an exact
+        but slower raster), which must be 0."""
+        from libnativecpurenderer_amd import sharding
+        ctx = self.ctx
+        out = {"verified": None, "warm_failures": int(ctx.warm_failure_count())}
+        key = digest_key(self.cfg_name, self.cfg, last_i)
+        ref = load_digests().get(key)
+        if ref is None or (ref["W"], ref["H"], ref["band_rows"]) != (self.W, self.H, BAND_ROWS):
+            out["verify_note"] = f"no oracle digest for {key}"
+            return out
+        nb = (self.H + BAND_ROWS - 1) // BAND_ROWS
+        slots = self.slots_for(self.root_k) if self.nsh > 1 else None
+        owned = ([y0 // BAND_ROWS for y0, _ in sharding.owned_bands(self.H, self.nsh, self.me, slots=slots)]
+                 if self.nsh > 1 else list(range(nb)))
+        fo = self.frame_output
+        # the frame output on the device: the whole frame on the root of an RCCL
+        # gather; the host frame: whole too when every rank delivered its bands
+        # into it (drain + barrier before this runs)
+        dev_bands = list(range(nb)) if (self.world > 1 and self.comm is not None and self.rank == 0) else owned
+        host_bands = list(range(nb)) if (self.deliver == "bands" and self.world > 1) else dev_bands
+        checks = [("f64", "f64", ctx.get_buffer_numpy(), owned), ("depth", "depth", ctx.get_depth_buffer(), owned)]
+        if self.deliver != "bands":
+            checks.append(("frame_output", fo, ctx.get_frame_u8(), dev_bands))
+        if self.host is not None and self.rank == 0:   # the host frame of the last step
+            hb = np.asarray(self.host[last_i % 2].array()).reshape(-1)[:int(np.prod(ctx.frame_output_shape()))]
+            a = hb if fo == "yuv420p" else hb.reshape(ctx.frame_output_shape())
+            checks.append(("host_frame", fo, a, host_bands))
+        bad, n = [], 0
+        for what, kind, arr, bands in checks:
+            for b in bands:
+                n += 1
+                if band_digest(kind, arr, self.W, self.H, b) != ref[kind][b]:
+                    bad.append(f"{what}:band{b}")
+        out.update({"verified": not bad, "verify_digest": f"{os.path.relpath(DIGEST_FILE, ROOT)}[{key}]",
+                    "verified_bands": n, "verified_buffers": [c[0] for c in checks]})
+        if bad:
+            out["verify_mismatches"] = bad[:16]
+        if self.nsh == 1 and self.world == 1 and not self.cfg.get("animate"):
+            out["fragments_match_oracle"] = int(round(self.frags)) == ref["fragments"]
+        return out
+
     def run(self, steps, warmup, calibrate=False):
         import torch
         ctx, dist = self.ctx, self.dist
@@ -309,6 +394,7 @@ class Runner:
             t = torch.tensor([frags], dtype=torch.float64, device=self.rdev)
             dist.all_reduce(t)
             frags = float(t.item())
+        self.frags = frags
 
         # partition calibration (N>1, --root-slots auto): every candidate share
         # of rank 0 is timed over a few frames (max over ranks), the fastest kept
@@ -366,9 +452,10 @@ class Runner:
         kb = kernel_bytes(self.cfg, self.n_tri, path, share, self.frame_output)
         dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
-        # (2) timed region: K frames, HIP events only around the dominant kernel
-        #     (every EVENT_EVERY-th frame: each record leaves a few-us bubble on
-        #     the stream, so sampling keeps the headline close to the untimed rate)
+        # (2) timed region: K frames.  The dominant kernel is timed by its own
+        #     dispatch timestamps (hipExtLaunchKernel start/stop events bound to
+        #     the launch: no marker packets on the stream, the kernel's execution
+        #     time as rocprofv3's kernel trace has it) on every --event-every-th frame
         timing = not self.args.no_kernel_timing
         ctx.reset_kernel_timing()
         ctx.set_kernel_timing_filter("" if not timing else dom)
@@ -376,7 +463,7 @@ class Runner:
         warm0 = ctx.warm_batch_count()
         t0 = time.perf_counter()
         for i in range(steps):
-            ctx.enable_kernel_timing(timing and i % EVENT_EVERY == 0)
+            ctx.enable_kernel_timing(timing and i % self.args.event_every == 0)
             self.frame(i)
         self.drain()
         torch.cuda.synchronize()
@@ -386,19 +473,27 @@ class Runner:
         ctx.enable_kernel_timing(False)
         warm_frames = ctx.warm_batch_count() - warm0
         ms = dt / steps * 1e3
+        # the last timed frame against the oracle's digests (outside the timed region)
+        ver = self.verify(steps - 1)
+        if dist is not None:   # every rank's verdict: false if any rank mismatched
+            if self.max_over_ranks(1.0 if ver["verified"] is False else 0.0) > 0:
+                ver["verified"] = False
+            ver["warm_failures"] = int(self.max_over_ranks(float(ver["warm_failures"])))
         tot, cnt = ctx.get_kernel_timing(dom)
         dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
         achieved = kb[dom] / (dom_us * 1e-6) / 1e9
         B = algorithmic_bytes(self.cfg, self.n_tri, frame_out=self.frame_output)   # whole frame
         ksym = "k_tile_raster" if path == "ordered" else "k_vis"
-        traffic, traffic_src = load_pmc_traffic(self.cfg_name, self.nsh if self.world == 1 else 1,
-                                                slots if self.world == 1 else None, self.frame_output, ksym)
-        if self.world > 1:
-            traffic, traffic_src = None, None   # per-rank PMC passes are not taken on multi-GPU runs
+        # (at N>1 the PMC summary of rank 0's share, taken as an emulated share on one GPU)
+        traffic, traffic_src = load_pmc_traffic(self.cfg_name, self.nsh, slots, self.frame_output, ksym)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
                 "traffic_source": traffic_src or "none for this config/share (null)",
+                # the bytes the kernel physically moved (PMC) over the same kernel time
+                "traffic_frac": round(traffic / (dom_us * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4) if traffic else None,
                 "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
+                "kernel_us_source": (f"dispatch timestamps of every {self.args.event_every}th timed launch "
+                                     f"({cnt} launches)" if cnt else "breakdown pass"),
                 "algorithmic_bytes_per_launch": kb[dom], "rank_share_of_frame": round(share, 6),
                 **frame_roofline(B, share, ms, self.world)}
         out = {
@@ -413,6 +508,7 @@ class Runner:
             "calib": calib,
             "warm_binned_frames": warm_frames,
             "clock_settle": {"ms": self.args.clock_settle_ms, "frames": self.settle_frames},
+            **ver,
         }
         if path == "ordered" and self.cfg.get("soup", (0, 0, None))[2] is not None:
             # C5: the blend loop is bound by f64 VALU issue, not by HBM (per
@@ -427,7 +523,7 @@ class Runner:
         return out
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -448,6 +544,8 @@ def main():
                          "bands: every rank copies its own bands straight into one shared pinned host frame "
                          "(DeliverFrameBands, no GPU gather: each GPU's PCIe link carries its share)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="time without per-kernel HIP events")
+    ap.add_argument("--event-every", type=int, default=EVENT_EVERY,
+                    help="time the dominant kernel's launch (its dispatch timestamps) on every k-th timed frame")
     ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
     ap.add_argument("--lib", default=None,
                     help="experiment: load another build of the library (tools/exp A/B and probe builds)")
@@ -466,7 +564,11 @@ def main():
                          "rank (SetShardSlots); 'equal' = SetShard; 'auto' (N>1) times candidates and keeps the "
                          "fastest -- the root also receives every other rank's bands, so it gets less to render "
                          "when the gather dominates")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
     if args.lib:
         from libnativecpurenderer_amd import _lib
         _lib.LIB_PATH = os.path.abspath(args.lib)
@@ -516,7 +618,12 @@ def main():
                                                                          "fragments_per_frame", "roofline",
                                                                          "raster_path", "kernel_us",
                                                                          "warm_binned_frames")},
+                          **{k: r[k] for k in VERIFY_KEYS if k in r},
                           **({"valu_roofline": r["valu_roofline"]} if "valu_roofline" in r else {})}
+            if name == "c3_1080p" and dl == "none" and not args.no_cpu_baseline:
+                # the metric's literal configuration gets its own CPU baseline (same oracle, same pinning)
+                extra[key]["cpu_baseline"] = cpu_baseline(sub.cfg, sub.xy, sub.z, sub.c, budget_s=5.0)
+                extra[key]["vs_cpu"] = round(r["value"] / extra[key]["cpu_baseline"]["value"], 1)
             if dl == "host":
                 extra[key]["host_frame_bytes"] = int(np.prod(sub.ctx.frame_output_shape()))
                 same = res if name == args.config and args.deliver == "none" else extra.get(name)
@@ -561,7 +668,10 @@ def main():
         "raster_path": res["raster_path"],
         "kernel_us": res["kernel_us"],
         "clock_settle": res["clock_settle"],
-        "kernel_us_note": f"per-launch averages from a breakdown pass with events around every kernel; the timed region records events around the dominant kernel on every {EVENT_EVERY}th frame (roofline.kernel_us)",
+        **{k: res[k] for k in VERIFY_KEYS if k in res},
+        "kernel_us_note": "kernel_us: per-launch averages from a breakdown pass with events around every kernel "
+                          "(the rasters by their dispatch timestamps); roofline.kernel_us: the dominant kernel's "
+                          "dispatch timestamps over the timed region (roofline.kernel_us_source)",
     }
     if "valu_roofline" in res:
         result["valu_roofline"] = res["valu_roofline"]

@@ -153,7 +153,8 @@ void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW:
 void SetWarmBinning(RenderContext* ctx, i64 mode);                       /* NEW: one-pass binning of a repeat draw 0 auto, 1 on, 2 off */
 i64 GetWarmBatchCount(RenderContext* ctx);                               /* NEW (testing): batches binned warm */
 void SetWarmFaultInjection(RenderContext* ctx, i64 mode);                /* NEW (testing): fault in the next warm batch
-                                 1 range overflow, 2 withheld token, 3 dropped pairs (the frame must stay exact) */
+                                 1 range overflow, 2 withheld token, 3 dropped pairs, 4 binning delayed past the
+                                 raster's token wait (the frame must stay exact) */
 i64 GetWarmFailureCount(RenderContext* ctx);                             /* NEW (testing): warm batches that failed a check */
 void SetSplitLimits(RenderContext* ctx, i64 splitAt, i64 dslice);       /* NEW: dense-tile split limits (0: defaults) */
 
@@ -177,7 +178,11 @@ void FreeHostBuffer(void* p);
 i64 DeliverFrameBands(RenderContext* ctx, iu8* host); /* §8e: this rank's bands of its frame output straight into
                                                        their places in a host frame (every rank into the same one:
                                                        assembled by each GPU's own PCIe link, no GPU ingress);
-                                                       async on the gather stream -> ticket for WaitFrameDelivered */
+                                                       async on the gather stream -> ticket for WaitFrameDelivered.
+                                                       `host` should be pinned (AllocHostBuffer /
+                                                       AllocSharedHostBuffer): small shares are then written by a
+                                                       copy kernel through its device address; any other host
+                                                       pointer takes the (slower) runtime copies */
 void* AllocSharedHostBuffer(const char* name, i64 bytes); /* pinned POSIX shared memory "/name" (one host frame for
                                                        the processes of a sharded frame) */
 void FreeSharedHostBuffer(void* p, i64 bytes);

@@ -283,6 +283,17 @@ void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b) {
     nr_timing_end_on(ctx, kid, a, b, ctx->stream);
 }
 
+void nr_timing_kernel(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b) {
+    *a = *b = nullptr;
+    if (!ctx->timing || !((ctx->timingMask >> kid) & 1ull)) return;
+    *a = ev_get(ctx);
+    *b = ev_get(ctx);
+}
+void nr_timing_kernel_done(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b) {
+    if (!a) return;
+    ctx->evPending.push_back({kid, {a, b}});
+}
+
 static void timing_collect(RenderContext* ctx) {
     if (ctx->evPending.empty()) return;
     NR_CHECK(hipStreamSynchronize(ctx->stream));

@@ -124,6 +124,11 @@ struct TriScratch {
     u64 warmFailures = 0;                   // warm batches that failed their checks (GetWarmFailureCount)
     std::vector<u64> warmBanned;            // buffers (uid) whose warm binning failed a check: binned cold
     int warmInject = 0;                     // testing: fault injected into the next warm batch (SetWarmFaultInjection)
+    // a warm binning beside the raster was handed off by its token only (no
+    // event the main stream waits on): before the main stream next writes a
+    // binning set or the schedule, it waits for the binning stream (evSide)
+    bool sideGated = false;
+    hipEvent_t evSide = nullptr;
 };
 
 enum NRKernelId { NRK_TRI_COUNT = 0, NRK_TRI_SCAN, NRK_TRI_EMIT, NRK_TRI_SORT, NRK_TILE_RANGES,
@@ -252,6 +257,12 @@ void nr_materialize_depth(RenderContext* ctx);
 void nr_materialize_tiles(RenderContext* ctx, bool color, bool depth);   // tile-granular pending clears
 void nr_ensure_depth(RenderContext* ctx);
 void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
+// Timing of one kernel by its own dispatch timestamps: the pair is handed to
+// hipExtLaunchKernel as its start / stop events (no marker packets around the
+// kernel, so the stream is not perturbed and the time is the kernel's
+// execution, as rocprofv3's kernel trace reports it), then queued by _done.
+void nr_timing_kernel(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
+void nr_timing_kernel_done(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);
 void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);
 void nr_fill_f64(hipStream_t s, f64* p, i64 n, f64 v);
 void nr_fill_u32(hipStream_t s, u32* p, i64 n, u32 v);

@@ -830,10 +830,17 @@ i64 DeliverFrameBands(RenderContext* ctx, iu8* host) {
     const i64 bands = (ctx->height + BAND - 1) / BAND;
     const int P = ctx->shardPeriod;
     const i64 full = ctx->height / BAND;   // bands [0, full) have BAND rows; band `full` (if any) is short
-    const bool viaKernel = owned_bytes(ctx, ctx->shard) <= BAND_KERNEL_MAX;
+    // The copy kernel writes through the host frame's device address, which
+    // only pinned (hipHostMalloc'd / registered) memory has: for any other host
+    // pointer (a numpy or malloc buffer) the runtime copies below take over
+    // (the failed lookup used to leave a null address to write to).
+    void* hdev = nullptr;
+    bool viaKernel = owned_bytes(ctx, ctx->shard) <= BAND_KERNEL_MAX;
+    if (viaKernel && (hipHostGetDevicePointer(&hdev, host, 0) != hipSuccess || !hdev)) {
+        (void)hipGetLastError();   // (an answer: not pinned -- not a failure to latch)
+        viaKernel = false;
+    }
     if (viaKernel) {
-        void* hdev = nullptr;
-        NR_CHECK(hipHostGetDevicePointer(&hdev, host, 0));
         bool vec = (reinterpret_cast<uintptr_t>(hdev) | reinterpret_cast<uintptr_t>(frame)) % 16 == 0;
         for (i64 b = 0; b < bands && vec; ++b) {
             i64 off[3], len[3];
@@ -900,7 +907,8 @@ void* AllocSharedHostBuffer(const char* name, i64 bytes) {
         nr_set_error_msg("AllocSharedHostBuffer: mmap failed");
         return nullptr;
     }
-    if (hipHostRegister(p, (size_t)bytes, hipHostRegisterPortable) != hipSuccess) {
+    // (mapped: DeliverFrameBands' copy kernel writes through its device address)
+    if (hipHostRegister(p, (size_t)bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
         (void)hipGetLastError();
         munmap(p, (size_t)bytes);
         nr_set_error_msg("AllocSharedHostBuffer: hipHostRegister failed");

@@ -477,7 +477,7 @@ constexpr int ORD_BIN_TILES = 16384;  // tiles of the binned ordered path (the r
 // are no-ops unless plan[3] (fits)
 void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, hipStream_t s, hipEvent_t stop);
 void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* off, const u32* plan, const f64* rec,
-                           int ntiles, hipStream_t s, hipEvent_t stop);
+                           int ntiles, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 // tb: the batch is that (immutable) TriangleBuffer, so its binning may overlap
 // the previous raster and a repeat draw is sized from its known totals;
 // callerOwned: the arrays are the caller's device memory (DrawTrianglesDevice),

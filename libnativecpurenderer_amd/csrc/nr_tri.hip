@@ -371,9 +371,10 @@ i64 GetWarmBatchCount(RenderContext* ctx) { return (i64)ctx->tri.warmBatches; }
 // New (testing): a fault in the next warm batch -- 1 its binning finds its
 // tiles over their ranges, 2 (a batch binned beside the raster) its token is
 // withheld (the raster's wait times out after 1 s), 3 it drops a workgroup's
-// pairs.  The raster must then run its fallback (k_vis WarmCheck): the frame
+// pairs, 4 (beside the raster) its binning is held back 1.5 s, so that it
+// lands after the raster's fallback.  The raster must then run its fallback (k_vis WarmCheck): the frame
 // stays exact and the failure is latched (GetWarmFailureCount, the error).
-void SetWarmFaultInjection(RenderContext* ctx, i64 mode) { ctx->tri.warmInject = (int)(mode >= 0 && mode <= 3 ? mode : 0); }
+void SetWarmFaultInjection(RenderContext* ctx, i64 mode) { ctx->tri.warmInject = (int)(mode >= 0 && mode <= 4 ? mode : 0); }
 // New (testing): warm batches whose checks failed so far (read at API calls).
 i64 GetWarmFailureCount(RenderContext* ctx) {
     NR_CHECK(hipSetDevice(ctx->device));

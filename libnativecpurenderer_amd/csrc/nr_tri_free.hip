@@ -550,14 +550,16 @@ __global__ __launch_bounds__(256) void k_free_emit(const BinParams bp, const u32
 // The set's pair cursors are not reset between warm batches: the epoch-th
 // warm batch of one schedule on this set finds cur[t] = epoch * count(t) and
 // takes slots from there (cursor - epoch * count, count = off[t + 1] - off[t]).
-// Checks (wstat, beside the cursors): a tile found over its range stores the
-// batch's tag in wstat[WS_TAG] (its excess pairs are dropped), and every
-// workgroup adds its pair total to wstat[WS_SUM] (zeroed with the cursors),
-// which after the e-th warm batch must equal
-// (e + 1) * the schedule's pairs -- so an undercount anywhere is seen too.
-// k_vis reads both before it trusts the lists (WarmCheck).  `inject` (tests
-// only, SetWarmFaultInjection): 1 shifts the epoch (every touched tile out of
-// its range), 3 drops workgroup 0's pairs (an undercount).
+// Checks: a tile found over its range stores the batch's tag in
+// wstat[WS_TAG] (beside the cursors; its excess pairs are dropped), and k_vis
+// checks every tile's cursor before it trusts the tile's list: after the e-th
+// warm batch cur[t] must be (e + 1) * count(t), so an undercount or an
+// overcount of that tile is seen there, and only that tile falls back
+// (WarmCheck; round 6 -- until round 5 every binning workgroup added its pair
+// total to one global sum word: ~4000 atomics on one address, 3.5 us of the
+// 1080p frame, profiles/r05/ab_pair_sum.txt).  `inject` (tests only,
+// SetWarmFaultInjection): 1 shifts the epoch (every touched tile out of its
+// range), 3 drops workgroup 0's pairs (an undercount of its tiles).
 // Can a cluster (user-space box {xmin, ymin, xmax, ymax}, TriangleBuffer::cbox)
 // put a pair into an owned tile?  Its corners' screen positions bound every
 // vertex's (the affine map's rounded products and sums are monotone in x and
@@ -587,7 +589,10 @@ __device__ __forceinline__ bool cluster_may_touch(const BinParams& bp, const f64
     return ty1 >= ty0 + 64;
 }
 
-enum { WS_SUM = 0, WS_TAG = 1 };   // the warm checks' words, right after a set's ntiles cursors
+// the warm checks' words, right after a set's ntiles cursors: WS_TAG the tag of
+// a batch with a tile over its range, WS_REP the tag of the last batch whose
+// failure a k_vis workgroup reported (one report per batch)
+enum { WS_REP = 0, WS_TAG = 1 };
 template <bool LDSH>
 __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32* __restrict__ off,
                                                   u32* __restrict__ cur, u32* __restrict__ list,
@@ -595,7 +600,6 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
                                                   const f64* __restrict__ cbox, const u32* __restrict__ blocks,
                                                   u32 inject) {
     extern __shared__ u32 hist[];
-    __shared__ u32 wgPairs;
     const int tid = threadIdx.x;
     if (inject == 1) epoch += 7;
     if (inject == 3 && blockIdx.x == 0) return;
@@ -618,7 +622,6 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
     // a workgroup none of whose clusters reaches an owned tile has nothing to do
     // (most of them on a sharded frame's rank)
     if (cbox && !__syncthreads_or(anyc ? 1 : 0)) return;
-    if (tid == 0) wgPairs = 0;
     // (loading the positions before the cluster test -- one latency round
     // less, all bytes -- was not faster, round 4)
     f64 pxy[TPT][6];
@@ -628,9 +631,8 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
         if (cl[k] && t < bp.src.n) load_tri_xy(bp.src.xy, t, pxy[k]);
     }
     if (LDSH) for (int b = tid; b < hbins; b += 256) hist[b] = 0;
-    __syncthreads();   // (hist and wgPairs zeroed)
+    if (LDSH) __syncthreads();   // (hist zeroed)
     u64 rk[TPT];
-    u32 myPairs = 0;
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
@@ -644,15 +646,10 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
         rk[k] = pack_rect(tx0, tx1, ty0, ty1);
         for (int ty = ty0; ty <= ty1; ++ty) {
             if (!owned_row(ty, bp.period, bp.mask)) continue;
-            myPairs += (u32)(tx1 - tx0 + 1);
             if (!LDSH) continue;
             const int hrow = owned_ord(bp, ty) * bp.tiles_x;
             for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[hrow + tx], 1u);
         }
-    }
-    {   // the workgroup's pair total (one global atomic)
-        const u32 wp = wave_scan(myPairs, tid & 63);
-        if ((tid & 63) == 63 && wp) atomicAdd(&wgPairs, wp);
     }
     if (LDSH) {
         __syncthreads();
@@ -670,8 +667,7 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
             }
         }
     }
-    __syncthreads();   // (LDS ranges reserved; wgPairs complete)
-    if (tid == 0 && wgPairs) atomicAdd(&wstat[WS_SUM], wgPairs);
+    if (LDSH) __syncthreads();   // (LDS ranges reserved)
 #pragma unroll
     for (int k = 0; k < TPT; ++k) {
         const i64 t = base + k * 256 + tid;
@@ -993,22 +989,36 @@ constexpr int KS = TW + 1;        // padded row stride of the LDS tile keys
 // pair density -- the variant without it keeps fewer registers live for sliver meshes.
 // NT: workgroup size (VWG, or 2 * VWG for batches with few pairs, whose dense
 // items are latency-bound: more waves per item).
-// The checks of a warm batch (k_bin_warm): wstat = {pair sum of the set's
-// warm batches since its cursors were zeroed, tag of a batch that found a tile
-// over its range}; the lists are trusted when the sum == expect, the tag word
-// != this batch's tag and the plan says it fits (plan[3] == 0: the binning's token never
-// came, k_gate_wait).  Otherwise the raster runs its work items over EVERY
-// triangle of the batch instead of the tile lists -- slow, but the same frame
-// bit for bit (a triangle that misses a tile adds nothing to it) -- and
-// workgroup 0 reports the reason in host-mapped *hfail (1 binning check, 2
-// token timeout; nr_settle latches an error and drops the schedule).  wstat
-// null: a cold batch (plan[3] == 0 there: the batch does nothing, the host
-// re-runs it).
+// The checks of a warm batch (k_bin_warm).  Batch-wide: the tag word
+// wstat[WS_TAG] != this batch's tag (no tile over its range) and the plan says
+// it fits (plan[3] == 0: the binning's token never came, k_gate_wait);
+// otherwise the raster runs its work items over EVERY triangle of the batch
+// instead of the tile lists -- slow, but the same frame bit for bit (a
+// triangle that misses a tile adds nothing to it).  Per tile: the tile's
+// cursor == mult * its count (mult = epoch + 1: the cursors run on across a
+// schedule's warm batches, k_bin_warm); otherwise only that tile's items run
+// over every triangle.  The first workgroup to see a failure (wstat[WS_REP]
+// exchanged for the batch's tag) reports it in host-mapped *hfail (reason 1 a
+// tile over its range, 2 token timeout, 3 a tile's count wrong; nr_settle
+// latches an error and drops the schedule).  wstat null: a cold batch
+// (plan[3] == 0 there: the batch does nothing, the host re-runs it).
 struct WarmCheck {
-    const u32* wstat;
-    u32 tag, expect;
+    u32* wstat;
+    const u32* cur;   // the set's cursors
+    const u32* off;   // the schedule's tile offsets
+    u32 tag, mult;
     u32* hfail;
 };
+
+// One report per failed warm batch (see WarmCheck): words 1..3 for the
+// message, then the reason.
+__device__ __forceinline__ void warm_report(const WarmCheck& wc, u32 why, u32 a, u32 b, u32 c) {
+    if (__hip_atomic_exchange(&wc.wstat[WS_REP], wc.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == wc.tag) return;
+    __hip_atomic_store(&wc.hfail[1], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&wc.hfail[2], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&wc.hfail[3], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&wc.hfail[0], why, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
@@ -1033,15 +1043,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
     bool fb = false;   // fallback: every triangle of the batch against every tile (WarmCheck)
     if (wc.wstat) {
         const u32 wt = __hip_atomic_load(&wc.wstat[WS_TAG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u32 ws = __hip_atomic_load(&wc.wstat[WS_SUM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fb = !plan[3] || wt == wc.tag || ws != wc.expect;
-        if (fb && blockIdx.x == 0 && threadIdx.x == 0) {   // (the words read, for the message; then the reason)
-            __hip_atomic_store(&wc.hfail[1], ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&wc.hfail[2], wc.expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&wc.hfail[3], (wt == wc.tag ? 1u : 0u) | (plan[3] ? 0u : 2u), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&wc.hfail[0], plan[3] ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        fb = !plan[3] || wt == wc.tag;
+        if (fb && blockIdx.x == 0 && threadIdx.x == 0) warm_report(wc, plan[3] ? 1u : 2u, ~0u, wt, wc.tag);
     } else if (!plan[3]) {
         return;
     }
@@ -1053,6 +1056,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
     // grid-stride over the work items (the grid is sized from a capacity
     // bound, not from the item count, so no host sync is needed)
     uint4 dnext = blockIdx.x < nitems ? items[blockIdx.x] : make_uint4(0, 0, 0, 0);
+    u32 badTile = ~0u;   // a tile of this workgroup's whose cursor check failed (WarmCheck)
 #if NR_PROBE
     u64 pr_t0 = 0;
     u32 pr_item = ~0u;
@@ -1074,7 +1078,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
         u32 ls = d.y, le = d.z;
         const u32 nsl = d.w & 0xFFFFu;   // slices of the tile (d.w >> 16: this item's slice)
         const bool multi = nsl > 1;
-        if (fb) {   // this item's slice of all n triangles (never empty: a split tile has n >= its pairs > nsl)
+        bool fbt = fb;   // this tile's list is not trusted (WarmCheck)
+        if (wc.wstat && !fb) {
+            // (uniform values: scalar registers, nothing kept in VGPRs across the item)
+            const u32 cnt = __builtin_amdgcn_readfirstlane(wc.off[tile + 1] - wc.off[tile]);
+            const u32 cu = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&wc.cur[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            fbt = cu != wc.mult * cnt;
+            if (fbt) badTile = (u32)tile;   // (reported after the item loop: no report code live in it)
+        }
+        if (fbt) {   // this item's slice of all n triangles (never empty: a split tile has n >= its pairs > nsl)
             const u64 n = (u64)fp.src.n, k = d.w >> 16;
             ls = (u32)(k * n / nsl);
             le = (u32)((k + 1) * n / nsl);
@@ -1151,7 +1164,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
             const int ln = opaque_tid() & 63;   // (formed here: the lane index is not kept live across the item)
             const u32 b = ls + c * cs + ln;
             const u32 i = c < nch && (u32)ln < cs && b < le ? b : ls;
-            return fb ? i : list[i];   // (fallback: the slice's triangle ids themselves)
+            return fbt ? i : list[i];   // (fallback: the slice's triangle ids themselves)
         };
         // chunk c + NWV's triangle (loaded) and chunk c + 2 NWV's (in flight)
         u32 pt = list_at(wave), ptn = list_at(wave + NWV);
@@ -1371,6 +1384,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
 #if NR_PROBE
     if (tid == 0 && pr_item != ~0u) probe_item(pr_item, pr_d, pr_t0, __builtin_amdgcn_s_memrealtime(), NT);
 #endif
+    if (badTile != ~0u && tid == 0)
+        warm_report(wc, 3u, badTile, wc.cur[badTile], wc.mult * (wc.off[badTile + 1] - wc.off[badTile]));
     if (COUNT) {
         __syncthreads();
         atomicAdd(&sFrag, myFrags);
@@ -1401,7 +1416,7 @@ struct VisArgs {
 
 template <int Z, bool C, bool G>
 void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
-                hipEvent_t stop) {
+                hipEvent_t start, hipEvent_t stop) {
     const WarmCheck wc = va.wc;
     // coop pass when the previous batch had more than COOP_PAIRS tiles per
     // triangle (large triangles), or when there is no history
@@ -1411,7 +1426,7 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
     // its dense items run at low occupancy and are latency-bound
     const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < WIDE_HEAVY;
 #define NR_VIS(CO, NTT, ...)                                                                                       \
-    hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, nullptr, stop, 0, fp, va.items,  \
+    hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, start, stop, 0, fp, va.items,    \
                           va.list, sc.kslot, sc.fdone, va.plan, wc)
     if (wide) {
         if (coop) NR_VIS(1, 2 * VWG, false, G, true, 2 * VWG);
@@ -1426,16 +1441,19 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
 
 template <int Z, bool G>
 void launch_vis_z(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
-                  hipEvent_t stop) {
-    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, va, grid, s, stop);
-    else launch_vis<Z, false, G>(fp, sc, va, grid, s, stop);
+                  hipEvent_t start, hipEvent_t stop) {
+    if (fp.fragCounter) launch_vis<Z, true, G>(fp, sc, va, grid, s, start, stop);
+    else launch_vis<Z, false, G>(fp, sc, va, grid, s, start, stop);
 }
 
 static void launch_vis_any(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
-                           hipEvent_t stop, int zmode, bool g) {
-    if (zmode == 1) { if (g) launch_vis_z<1, true>(fp, sc, va, grid, s, stop); else launch_vis_z<1, false>(fp, sc, va, grid, s, stop); }
-    else if (zmode == 2) { if (g) launch_vis_z<2, true>(fp, sc, va, grid, s, stop); else launch_vis_z<2, false>(fp, sc, va, grid, s, stop); }
-    else { if (g) launch_vis_z<0, true>(fp, sc, va, grid, s, stop); else launch_vis_z<0, false>(fp, sc, va, grid, s, stop); }
+                           hipEvent_t start, hipEvent_t stop, int zmode, bool g) {
+#define NR_VZ(ZM) (g ? launch_vis_z<ZM, true>(fp, sc, va, grid, s, start, stop) \
+                     : launch_vis_z<ZM, false>(fp, sc, va, grid, s, start, stop))
+    if (zmode == 1) NR_VZ(1);
+    else if (zmode == 2) NR_VZ(2);
+    else NR_VZ(0);
+#undef NR_VZ
 }
 
 // Events of a batch carried by the kernels' own completion signals
@@ -1487,6 +1505,25 @@ static hipEvent_t sync_event() {
     return e;
 }
 
+// A warm binning beside the raster hands off to the raster through its token
+// only.  Should the raster's wait time out (a binning delayed by over a second,
+// or serialised dispatch), the raster falls back and finishes while that
+// binning may still be queued or running on the binning stream, and nothing
+// orders later main-stream work after it.  So before the main stream writes a
+// binning set or the warm schedule itself -- a binning on the main stream
+// (inline warm, or a cold batch binned in line) or sched_capture's copies into
+// the schedule every warm binning reads -- it waits for everything enqueued on
+// the binning stream so far.  Steady state (always beside, or
+// always inline) never takes this wait.
+static void main_after_side_binning(RenderContext* ctx) {
+    TriScratch& sc = ctx->tri;
+    if (!sc.sideGated) return;
+    if (!sc.evSide) sc.evSide = sync_event();
+    NR_CHECK(hipEventRecord(sc.evSide, nr_bin_stream_for(ctx->device)));
+    NR_CHECK(hipStreamWaitEvent(ctx->stream, sc.evSide, 0));
+    sc.sideGated = false;
+}
+
 // Enqueues one batch with binning outputs in set `si`.  exact: read the
 // pair/item totals back (host sync) and allocate exactly; otherwise size the
 // list from the previous batch, let the plan kernel check it on the device
@@ -1519,6 +1556,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
     const bool g = src.gouraud != 0;
     if (!F.evBin) { F.evBin = sync_event(); F.evVis = sync_event(); }
+    if (sb == sa) main_after_side_binning(ctx);
     // the set's buffers are rewritten (binning stream) only after the raster
     // that last read them; a regrow frees them, so the host waits for it then
     if (F.visRecorded && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, F.evVis, 0));
@@ -1715,19 +1753,20 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
 
     bool visDone = false;
     if (ordered) {   // one workgroup per tile, its list sorted in LDS
-        nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
+        nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = !e1;
-        launch_ordered_binned(fp, F.flist, F.foff, F.dplan, F.frec, ntiles, sa, vs ? F.evVis : nullptr);
+        launch_ordered_binned(fp, F.flist, F.foff, F.dplan, F.frec, ntiles, sa, e0, vs ? F.evVis : e1);
         NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+        nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
     } else if (grid > 0) {
-        nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
+        nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = !e1;
-        hipEvent_t st = vs ? F.evVis : nullptr;
-        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, 0u, 0u, nullptr}}, grid, sa, st, zmode, g);
+        hipEvent_t st = vs ? F.evVis : e1;
+        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, nullptr, nullptr, 0u, 0u, nullptr}}, grid, sa, e0, st,
+                       zmode, g);
         NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+        nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
     }
     if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
@@ -1748,11 +1787,15 @@ static bool warm_on(const TriScratch& sc) { return sc.warmMode != 2; }
 // raster HBM time to share -- for frame shares of >= 4 M pixels (C3 at 4K
 // 0.130 -> 0.124 ms, its 2-way share 0.092 -> 0.077 ms;
 // profiles/r05/ab_warm_beside.txt).  NR_WARM_INLINE: 1 always inline, 0
-// always beside (A/B).
+// always beside (A/B); inline by default under AMD_SERIALIZE_KERNEL.
 static bool warm_inline(i64 n, int period, u64 mask, i64 W, i64 H) {
     static const int v = [] {
         const char* e = getenv("NR_WARM_INLINE");
-        return e ? atoi(e) : 2;
+        if (e) return atoi(e);
+        // serialised dispatch: a binning beside the raster could not start
+        // until the raster's token wait gave up (a second per frame)
+        const char* ser = getenv("AMD_SERIALIZE_KERNEL");
+        return ser && atoi(ser) != 0 ? 1 : 2;
     }();
     if (v != 2) return v != 0;
     const u64 m = period >= 64 ? mask : (mask & ((1ull << period) - 1ull));
@@ -1771,6 +1814,7 @@ static void sched_capture(RenderContext* ctx, TriScratch::FreeSet& F, const BinK
     if (!warm_on(sc) || !tb) return;
     auto& S = sc.sched;
     hipStream_t sa = ctx->stream;
+    main_after_side_binning(ctx);   // (a late warm binning may still read S.off)
     S.valid = false;
     if (S.off_cap < (size_t)ntiles + 1 || S.items_cap < std::max<size_t>(items, 1) || !S.dplan) {
         NR_CHECK(hipStreamSynchronize(sa));   // a queued warm batch may still read the old arrays
@@ -1814,20 +1858,25 @@ static void warm_poll(RenderContext* ctx) {
     if (!sc.hfail) return;
     const u32 f = __atomic_load_n(sc.hfail, __ATOMIC_ACQUIRE);
     if (!f) return;
-    const u32 sum = __atomic_load_n(&sc.hfail[1], __ATOMIC_ACQUIRE), want = __atomic_load_n(&sc.hfail[2], __ATOMIC_ACQUIRE);
-    const u32 why = __atomic_load_n(&sc.hfail[3], __ATOMIC_ACQUIRE);
+    const u32 w1 = __atomic_load_n(&sc.hfail[1], __ATOMIC_ACQUIRE), w2 = __atomic_load_n(&sc.hfail[2], __ATOMIC_ACQUIRE);
+    const u32 w3 = __atomic_load_n(&sc.hfail[3], __ATOMIC_ACQUIRE);
     __atomic_store_n(sc.hfail, 0u, __ATOMIC_RELEASE);
     ++sc.warmFailures;
-    if (f == 1 && sc.sched.valid) sc.warmBanned.push_back(sc.sched.tbUid);
+    if (f != 2 && sc.sched.valid) sc.warmBanned.push_back(sc.sched.tbUid);
     sc.sched.valid = false;
     char msg[320];
     if (f == 2)
         snprintf(msg, sizeof msg, "triangle batch: a raster's wait for its warm binning timed out; the batch was "
-                                  "rasterised from all its triangles");
+                                  "rasterised from all its triangles (under serialised kernel dispatch -- a "
+                                  "profiler's counter passes, AMD_SERIALIZE_KERNEL -- set NR_WARM_INLINE=1)");
+    else if (f == 1)
+        snprintf(msg, sizeof msg, "triangle batch: a warm binning put a tile over its range (tag %u of batch %u); the "
+                                  "batch was rasterised from all its triangles and the buffer bins cold from now on",
+                 w2, w3);
     else
-        snprintf(msg, sizeof msg, "triangle batch: a warm binning failed its checks (tile over its range: %u, pair "
-                                  "sum %u, expected %u); the batch was rasterised from all its triangles and the "
-                                  "buffer bins cold from now on", why & 1u, sum, want);
+        snprintf(msg, sizeof msg, "triangle batch: a warm binning gave tile %u %u pairs, expected %u; that tile was "
+                                  "rasterised from all the batch's triangles and the buffer bins cold from now on",
+                 w1, w2, w3);
     nr_set_error_msg(msg);
 }
 
@@ -1850,6 +1899,14 @@ static void warm_poll(RenderContext* ctx) {
 // reports, WarmCheck.)
 __global__ void k_gate_signal(u32* __restrict__ gate, u32 tok) {
     if (threadIdx.x == 0) __hip_atomic_store(gate, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Testing (SetWarmFaultInjection 4): holds the binning stream for 1.5 s before
+// a warm binning, so that the raster's token wait (1 s) gives up first and the
+// binning lands after the raster's fallback (one thread, bounded).
+__global__ void k_delay_binning() {
+    if (threadIdx.x != 0) return;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 150000000ull) __builtin_amdgcn_s_sleep(127);
 }
 __global__ void k_gate_wait(const u32* __restrict__ gate, u32 tok, const u32* __restrict__ splan,
                             u32* __restrict__ gplan) {
@@ -1943,12 +2000,13 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     sc.fnext = (sc.fnext + 1) % BIN_SETS;
     TriScratch::FreeSet& F = sc.fset[si];
     if (!F.evBin) { F.evBin = sync_event(); F.evVis = sync_event(); }
+    if (sb == sa) main_after_side_binning(ctx);
     if (!sc.hfail) {
         NR_CHECK(hipHostMalloc((void**)&sc.hfail, 4 * sizeof(u32), hipHostMallocMapped | hipHostMallocCoherent));
         for (int k = 0; k < 4; ++k) sc.hfail[k] = 0;
         NR_CHECK(hipHostGetDevicePointer((void**)&sc.dfail, sc.hfail, 0));
     }
-    // cursors [0, ntiles), then the batch checks {error tag, pair sum} (WarmCheck)
+    // cursors [0, ntiles), then the batch checks {report tag, error tag} (WarmCheck)
     const size_t tneed = std::max<size_t>((size_t)ntiles + 2, TILE_ARR);
     const bool grow = F.ftile_cap < tneed || !F.fcnt || F.flist_cap < std::max<size_t>(S.pairs, 1) ||
                       sc.kslot_cap < std::max<size_t>(S.split, 1) * (TH * TW) || sc.fdone_cap < (size_t)ntiles + 1;
@@ -1982,7 +2040,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     // cursors: epoch e of this schedule on this set (k_bin_warm); zeroed for a
     // new schedule, after a cold batch on the set, or before they could wrap
     if (F.curGen != S.gen || (u64)(F.curEpoch + 1) * std::max<u32>(S.pairs, 1) >= 0xF0000000ull) {
-        NR_CHECK(hipMemsetAsync(F.fcur, 0, ((size_t)ntiles + 1) * sizeof(u32), sb));   // (and the pair sum)
+        NR_CHECK(hipMemsetAsync(F.fcur, 0, ((size_t)ntiles + 2) * sizeof(u32), sb));   // (and the check words)
         F.curGen = S.gen;
         F.curEpoch = 0;
     }
@@ -2000,6 +2058,10 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         // it -- that raster's wait then times out (seen with a cold-batch gate
         // on a busy device, profiles/r05/ab_cold_gate.txt)
         NR_CHECK(hipMemsetAsync(F.gate, 0, 4 * sizeof(u32), sb));
+        // and done before the first k_gate_wait (main stream) reads the word:
+        // uninitialised memory holding a token would let the raster go early
+        // (once per set)
+        NR_CHECK(hipStreamSynchronize(sb));
         F.gateTok = 0;
     }
     const bool xs = sb != sa && !e1 && !gated;
@@ -2007,7 +2069,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const u32 epoch = F.curEpoch++;
     if (++sc.warmTag == 0) sc.warmTag = 1;
     const u32 tag = sc.warmTag;
-    u32* const wstat = F.fcur + ntiles;   // {pair sum, error tag} (WS_SUM, WS_TAG)
+    u32* const wstat = F.fcur + ntiles;   // {report tag, error tag} (WS_REP, WS_TAG)
     const int inject = sc.warmInject;
     sc.warmInject = 0;
     // cluster culling of the rank's tile rows, and only the schedule's active blocks launched
@@ -2015,6 +2077,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const bool useBlocks = cbox && S.blocksGen == S.gen;
     const u32* blocks = useBlocks ? S.blocks : nullptr;
     const int grid = useBlocks ? (int)S.nblocks : gb;
+    if (inject == 4 && gated) hipLaunchKernelGGL(k_delay_binning, dim3(1), dim3(64), 0, sb);
     if (grid > 0) {
         if (ldsh)
             hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(grid), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
@@ -2037,6 +2100,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
                            F.gplan);
         NR_CHECK(hipGetLastError());
         visPlan = F.gplan;
+        sc.sideGated = true;
     } else if (sb != sa) {
         if (!xs) NR_CHECK(hipEventRecord(F.evBin, sb));
         NR_CHECK(hipStreamWaitEvent(sa, F.evBin, 0));
@@ -2046,13 +2110,13 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
     bool visDone = false;
     if (S.nitems > 0) {
-        nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
+        nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = !e1;
-        const WarmCheck wc{wstat, tag, (epoch + 1) * S.pairs, sc.dfail};
-        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa,
-                       vs ? F.evVis : nullptr, zmode, fp.src.gouraud != 0);
+        const WarmCheck wc{wstat, F.fcur, S.off, tag, epoch + 1, sc.dfail};
+        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa, e0,
+                       vs ? F.evVis : e1, zmode, fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
-        nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+        nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
         visDone = vs;
     }
     if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));

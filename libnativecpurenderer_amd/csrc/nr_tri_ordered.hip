@@ -493,23 +493,24 @@ __global__ __launch_bounds__(SORT_T) void k_tile_sort(const u32* __restrict__ of
 
 template <bool G, bool D, bool C, bool B>
 void launch_raster(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles, hipStream_t s,
-                   const f64* rec, const u32* plan, hipEvent_t stop) {
+                   const f64* rec, const u32* plan, hipEvent_t start, hipEvent_t stop) {
     if (fp.ipp == 4)
-        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, true, B>), dim3(ntiles), dim3(WG), 0, s, nullptr, stop, 0, fp, list,
+        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, true, B>), dim3(ntiles), dim3(WG), 0, s, start, stop, 0, fp, list,
                               ts, te, rec, plan);
     else
-        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, false, B>), dim3(ntiles), dim3(WG), 0, s, nullptr, stop, 0, fp,
+        hipExtLaunchKernelGGL((k_tile_raster<G, D, C, false, B>), dim3(ntiles), dim3(WG), 0, s, start, stop, 0, fp,
                               list, ts, te, rec, plan);
 }
 
 template <bool C, bool B>
 void launch_raster_c(const FrameParams& fp, const u32* list, const u32* ts, const u32* te, int ntiles,
-                     hipStream_t s, const f64* rec, const u32* plan = nullptr, hipEvent_t stop = nullptr) {
+                     hipStream_t s, const f64* rec, const u32* plan = nullptr, hipEvent_t start = nullptr,
+                     hipEvent_t stop = nullptr) {
     const bool g = fp.src.gouraud != 0, d = fp.depthTest != 0;
-    if (g && d) launch_raster<true, true, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
-    else if (g) launch_raster<true, false, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
-    else if (d) launch_raster<false, true, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
-    else launch_raster<false, false, C, B>(fp, list, ts, te, ntiles, s, rec, plan, stop);
+    if (g && d) launch_raster<true, true, C, B>(fp, list, ts, te, ntiles, s, rec, plan, start, stop);
+    else if (g) launch_raster<true, false, C, B>(fp, list, ts, te, ntiles, s, rec, plan, start, stop);
+    else if (d) launch_raster<false, true, C, B>(fp, list, ts, te, ntiles, s, rec, plan, start, stop);
+    else launch_raster<false, false, C, B>(fp, list, ts, te, ntiles, s, rec, plan, start, stop);
 }
 
 }  // namespace
@@ -519,9 +520,9 @@ void launch_tile_sort(const u32* off, u32* list, const u32* plan, int ntiles, hi
 }
 
 void launch_ordered_binned(const FrameParams& fp, const u32* list, const u32* off, const u32* plan, const f64* rec,
-                           int ntiles, hipStream_t s, hipEvent_t stop) {
-    if (fp.fragCounter) launch_raster_c<true, true>(fp, list, off, nullptr, ntiles, s, rec, plan, stop);
-    else launch_raster_c<false, true>(fp, list, off, nullptr, ntiles, s, rec, plan, stop);
+                           int ntiles, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+    if (fp.fragCounter) launch_raster_c<true, true>(fp, list, off, nullptr, ntiles, s, rec, plan, start, stop);
+    else launch_raster_c<false, true>(fp, list, off, nullptr, ntiles, s, rec, plan, start, stop);
 }
 
 void draw_ordered(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool callerOwned) {
@@ -642,11 +643,11 @@ void ordered_sorted_kernels(RenderContext* ctx, const TriSrc& src, const FramePa
         list = sc.vals[1];
     }
 
-    nr_timing_begin(ctx, NRK_TILE_RASTER, &e0, &e1);
-    if (fp.fragCounter) launch_raster_c<true, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
-    else launch_raster_c<false, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
+    nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
+    if (fp.fragCounter) launch_raster_c<true, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec, nullptr, e0, e1);
+    else launch_raster_c<false, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec, nullptr, e0, e1);
     NR_CHECK(hipGetLastError());
-    nr_timing_end(ctx, NRK_TILE_RASTER, e0, e1);
+    nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
 }
 
 }  // namespace

@@ -460,8 +460,9 @@ class RenderContext:
 
     def set_warm_fault_injection(self, mode: int):
         """Testing: a fault in the next warm batch (1 tile ranges overflow, 2
-        the binning's token is withheld, 3 a workgroup's pairs are dropped);
-        the frame must stay exact and the failure be latched."""
+        the binning's token is withheld, 3 a workgroup's pairs are dropped, 4
+        the binning is held back past the raster's token wait); the frame must
+        stay exact and the failure be latched."""
         lib.SetWarmFaultInjection(self._ptr, int(mode))
 
     def warm_failure_count(self) -> int:

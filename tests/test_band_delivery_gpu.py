@@ -91,3 +91,34 @@ def test_two_processes_assemble_one_shared_host_frame(fmt):
         assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} bytes differ"
     finally:
         host.close()
+
+
+class _Pageable:
+    """A plain numpy array as the host frame (not pinned: no device address)."""
+    def __init__(self, nbytes):
+        self.buf = np.full(nbytes, 0xA5, dtype=np.uint8)
+        self.ptr, self.nbytes = self.buf.ctypes.data, nbytes
+
+
+@pytest.mark.parametrize("fmt", ["rgb", "yuv420p"])
+def test_bands_into_pageable_host_memory(fmt):
+    """A host frame that is not pinned: the copy kernel cannot
+    write through a device address, so the runtime copies take the share --
+    the frame is still assembled exactly, and no error is latched."""
+    from libnativecpurenderer_amd import _lib
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    W, H, n = 320, 256, 2
+    xy, z, c = band_rank.mesh(W, H)
+    _lib.clear_error()
+    ctxs = []
+    for r in range(n):
+        ctx = R.RenderContext(W, H, False)
+        ctx.set_frame_format(fmt)
+        ctx.set_shard(n, r)
+        ctxs.append((ctx, R.TriangleBuffer(xy, c, z=z, gouraud=True)))
+    host = _Pageable(int(np.prod(ctxs[0][0].frame_output_shape())))
+    for ctx, buf in ctxs:
+        band_rank.render_frame(ctx, buf, 0)
+        ctx.wait_frame_delivered(ctx.deliver_frame_bands(host))
+    assert np.array_equal(host.buf, _reference(R, W, H, fmt, 0))
+    assert _lib.last_error() == "", _lib.last_error()

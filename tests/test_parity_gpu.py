@@ -747,6 +747,8 @@ def test_bench_multi_rank_orchestration_on_one_gpu(gpu, tmp_path, deliver):
     d = json.loads(line)
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 5
     assert set(d["config"]["partition_calibration_ms"]) >= {"equal", "3", "12"}
+    # the last timed frame of every rank checked against the oracle's digests
+    assert d["verified"] is True and d["warm_failures"] == 0, {k: d.get(k) for k in ("verify_mismatches", "verify_note")}
     if deliver == "bands":
         assert "shared pinned host frame" in d["config"]["frame_delivery"]
 

@@ -49,7 +49,7 @@ def _owned(H, n, r):
     return sharding.owned_rows(H, n, r)
 
 
-def _frames(fac, W, H, scene, nframes, shard=None, inject=None):
+def _frames(fac, W, H, scene, nframes, shard=None, inject=None, hook=None):
     xy, z, c = scene
     ctx = fac.context(W, H, False)
     if fac.name == "gpu":
@@ -62,6 +62,8 @@ def _frames(fac, W, H, scene, nframes, shard=None, inject=None):
     for k in range(nframes):
         if inject is not None and fac.name == "gpu" and k == inject[0]:
             ctx.set_warm_fault_injection(inject[1])
+        if hook is not None and fac.name == "gpu":
+            hook(k)
         ctx.set_color(0.1, 0.2, 0.3, 0.3 if k % 2 else 0.1)   # (non-uniform every other frame)
         ctx.set_depth_state(True, True)
         ctx.clear_depth()
@@ -116,3 +118,54 @@ def test_warm_fault_falls_back_exactly(gpu, oracle, mode, mesh_rc):
         assert w[6] > w[4], w   # warm again once a cold binning re-captured the schedule
     else:
         assert w[6] == w[3], w  # the buffer bins cold after a binning-check failure
+
+
+def test_late_binning_is_ordered_before_main_stream_reuse(gpu, oracle):
+    """a warm binning beside the raster that lands after the
+    raster's token wait gave up (fault 4: the binning stream is held 1.5 s).
+    The raster falls back (exact frame, one failure latched); the next batches
+    bin cold on the main stream (the readbacks leave it idle) into the same
+    binning sets and schedule the late binning writes -- they must wait for it
+    (main_after_side_binning), so every frame still equals the oracle's."""
+    from libnativecpurenderer_amd import _lib
+    W, H = 640, 400
+    scene = _scene(W, H)
+    want, _ = _frames(oracle, W, H, scene, 9)
+    _lib.clear_error()
+    got, ctx = _frames(gpu, W, H, scene, 9, inject=(3, 4))
+    for k, (g, o) in enumerate(zip(got, want)):
+        assert scenes.bits_equal(g["f64"], o["f64"]), f"frame {k}: {scenes.first_mismatch(g['f64'], o['f64'])}"
+        assert np.array_equal(g["depth"], o["depth"]), f"frame {k} depth"
+    assert ctx.warm_failure_count() == 1
+    assert "timed out" in _lib.last_error(), _lib.last_error()
+    w = ctx.warm_counts
+    assert w[8] > w[4], w   # warm again once a cold binning re-captured the schedule
+
+
+def test_fresh_gate_set_beside_a_busy_device(gpu, oracle):
+    """The token-word ordering of f1fb3a6 / ADVICE r05: a fresh context's
+    first warm batches beside the raster (new binning sets, whose token words
+    are zeroed on the binning stream) while the device is still busy with
+    another context's long blended raster -- no raster may time out waiting
+    for its token, and every frame is exact."""
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+    busy = R.RenderContext(1920, 1080, False)
+    bxy, bz, bc = scenes.triangle_soup(20000, 1920, 1080, 256, seed=9, alpha=(0.2, 0.8))
+    bbuf = R.TriangleBuffer(bxy, bc, z=bz)
+    busy.set_depth_state(True, False)
+
+    def hook(k):   # before the fresh context's frames 1.. (its first warm ones): ~ms of ordered raster queued
+        if k >= 1:
+            busy.set_color(0, 0, 0, 0)
+            for _ in range(4):
+                busy.draw_triangle_buffer(bbuf)
+    W, H = 640, 400
+    scene = _scene(W, H)
+    want, _ = _frames(oracle, W, H, scene, 6)
+    got, ctx = _frames(gpu, W, H, scene, 6, hook=hook)
+    for k, (g, o) in enumerate(zip(got, want)):
+        assert scenes.bits_equal(g["f64"], o["f64"]), f"frame {k}"
+        assert np.array_equal(g["depth"], o["depth"]), f"frame {k} depth"
+    assert ctx.warm_failure_count() == 0
+    assert ctx.warm_batch_count() >= 3
+    busy.flush()
