@@ -152,6 +152,8 @@ void SetPairCapacityOverride(RenderContext* ctx, i64 pairs);             /* NEW:
 void SetCoopRaster(RenderContext* ctx, i64 mode);                        /* NEW: k_vis variant 0 auto, 1 coop, 2 lane-only */
 void SetWarmBinning(RenderContext* ctx, i64 mode);                       /* NEW: one-pass binning of a repeat draw 0 auto, 1 on, 2 off */
 i64 GetWarmBatchCount(RenderContext* ctx);                               /* NEW (testing): batches binned warm */
+i64 GetLooseBatchCount(RenderContext* ctx);                              /* NEW (testing): of those, binned into the loose
+                                                                            ranges of a changed transform */
 void SetWarmFaultInjection(RenderContext* ctx, i64 mode);                /* NEW (testing): fault in the next warm batch
                                  1 range overflow, 2 withheld token, 3 dropped pairs, 4 binning delayed past the
                                  raster's token wait (the frame must stay exact) */

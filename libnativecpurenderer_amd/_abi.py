@@ -84,6 +84,7 @@ DEVICE_ABI = {
     "SetCoopRaster": (None, (P, L)),
     "SetWarmBinning": (None, (P, L)),
     "GetWarmBatchCount": (L, (P,)),
+    "GetLooseBatchCount": (L, (P,)),
     "ExecuteCommands": (L, (P, P, L, P, L)),
     "SetWarmFaultInjection": (None, (P, L)),
     "GetWarmFailureCount": (L, (P,)),

@@ -113,9 +113,18 @@ struct TriScratch {
         u32 nblocks = 0;
         u64 blocksGen = 0;                               // gen the list was built for (0: none)
         bool anyCull = true;                             // some cluster may lie off the owned tiles (else no device test)
+        // loose ranges (round 6): every tile's range widened to loose_cap(count)
+        // pairs, for a draw of the same buffer under a transform that moves no
+        // vertex more than LOOSE_PX from the key's (a moving scene: k_bin_warm
+        // into these ranges, k_vis slices each tile's actual count)
+        u32* off2 = nullptr; size_t off2_cap = 0;        // ntiles + 1 loose list offsets
+        u64 off2Gen = 0;                                 // gen they were formed for (0: none)
+        u64 pairs2 = 0;                                  // a bound of off2[ntiles] (list capacity)
     } sched;
     int warmMode = 0;                       // 0 automatic (NR_WARM), 1 on, 2 off (SetWarmBinning)
     u64 warmBatches = 0;                    // batches binned warm (GetWarmBatchCount)
+    u64 looseBatches = 0;                   // of those, into the loose ranges (GetLooseBatchCount)
+    std::vector<u64> looseBanned;           // buffers whose loose binning overflowed a tile: not binned loose again
     // warm-batch checks (k_vis WarmCheck): host-mapped word a raster sets when
     // a warm batch failed them (1 binning check, 2 token timeout), read by
     // nr_settle; the batch itself was rasterised from all its triangles
@@ -239,6 +248,10 @@ struct TriangleBuffer {
     // rank's tile rows without loading their triangles
     f64* cbox = nullptr;
     std::vector<f64> hcbox;   // (host copy: the warm schedule's active binning blocks are found on the host)
+    // user-space bounding box of every vertex {xmin, ymin, xmax, ymax} (NaN: a
+    // vertex is not finite): bounds how far a change of transform moves any
+    // vertex on screen (loose binning, nr_tri_free.hip)
+    f64 bbox[4] = {NAN, NAN, NAN, NAN};
 };
 constexpr int NR_CLUSTER = 64;
 

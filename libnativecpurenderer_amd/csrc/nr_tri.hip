@@ -321,6 +321,13 @@ TriangleBuffer* CreateTriangleBuffer(i64 n, const f64* xy, const f64* z, const f
         NR_CHECK(hipMalloc(&tb->cbox, cb.size() * sizeof(f64)));
         NR_CHECK(hipMemcpyAsync(tb->cbox, cb.data(), cb.size() * sizeof(f64), hipMemcpyHostToDevice, s));
         NR_CHECK(hipStreamSynchronize(s));
+        f64 b[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
+        for (size_t c = 0; c + 3 < cb.size(); c += 4) {
+            if (std::isnan(cb[c])) { b[0] = b[1] = b[2] = b[3] = NAN; break; }
+            b[0] = std::min(b[0], cb[c]); b[1] = std::min(b[1], cb[c + 1]);
+            b[2] = std::max(b[2], cb[c + 2]); b[3] = std::max(b[3], cb[c + 3]);
+        }
+        for (int k = 0; k < 4; ++k) tb->bbox[k] = b[k];
         tb->hcbox = std::move(cb);
     }
     return tb;
@@ -368,6 +375,8 @@ i64 GetFragmentCount(RenderContext* ctx) { return (i64)ctx->fragTotal; }
 void SetWarmBinning(RenderContext* ctx, i64 mode) { ctx->tri.warmMode = (int)(mode >= 0 && mode <= 2 ? mode : 0); }
 // New (testing): number of batches of this context binned warm so far.
 i64 GetWarmBatchCount(RenderContext* ctx) { return (i64)ctx->tri.warmBatches; }
+// New (testing): of those, batches binned into the loose ranges (a changed transform).
+i64 GetLooseBatchCount(RenderContext* ctx) { return (i64)ctx->tri.looseBatches; }
 // New (testing): a fault in the next warm batch -- 1 its binning finds its
 // tiles over their ranges, 2 (a batch binned beside the raster) its token is
 // withheld (the raster's wait times out after 1 s), 3 it drops a workgroup's

@@ -589,6 +589,32 @@ __device__ __forceinline__ bool cluster_may_touch(const BinParams& bp, const f64
     return ty1 >= ty0 + 64;
 }
 
+// Loose ranges (a moving scene): a tile of c pairs under the schedule's
+// transform gets room for loose_cap(c) under a transform that moves no vertex
+// more than LOOSE_PX (a quarter more, and 64 pairs for the triangles that move
+// in across its edges).  k_loose_off: one workgroup, off2 = exclusive scan of
+// loose_cap(off[t + 1] - off[t]), once per schedule.
+__host__ __device__ __forceinline__ u32 loose_cap(u32 c) { return c + c / 4 + 64; }
+__global__ __launch_bounds__(1024) void k_loose_off(const u32* __restrict__ off, u32* __restrict__ off2, int ntiles) {
+    __shared__ u32 wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int per = (ntiles + 1023) / 1024;
+    const int t0 = tid * per, t1 = min(ntiles, t0 + per);
+    u32 s = 0;
+    for (int t = t0; t < t1; ++t) s += loose_cap(off[t + 1] - off[t]);
+    const u32 inc = wave_scan(s, lane);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    u32 run = inc - s;
+    for (int k = 0; k < w; ++k) run += wsum[k];
+    for (int t = t0; t < t1; ++t) {
+        off2[t] = run;
+        run += loose_cap(off[t + 1] - off[t]);
+    }
+    if (t0 < t1 && t1 == ntiles) off2[ntiles] = run;   // (the last non-empty chunk)
+    if (ntiles == 0 && tid == 0) off2[0] = 0;
+}
+
 // the warm checks' words, right after a set's ntiles cursors: WS_TAG the tag of
 // a batch with a tile over its range, WS_REP the tag of the last batch whose
 // failure a k_vis workgroup reported (one report per batch)
@@ -598,10 +624,12 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
                                                   u32* __restrict__ cur, u32* __restrict__ list,
                                                   u32* __restrict__ wstat, u32 tag, u32 epoch,
                                                   const f64* __restrict__ cbox, const u32* __restrict__ blocks,
-                                                  u32 inject) {
+                                                  u32 inject, u32 loose) {
     extern __shared__ u32 hist[];
     const int tid = threadIdx.x;
-    if (inject == 1) epoch += 7;
+    // (fault 1 under loose ranges: every touched tile's count runs far past its range)
+    const u32 over = loose && inject == 1 ? 0x100000u : 0u;
+    if (inject == 1 && !loose) epoch += 7;
     if (inject == 3 && blockIdx.x == 0) return;
     // (blocks: the schedule's active blocks, warm_blocks; the others hold no
     // cluster that reaches an owned tile)
@@ -659,11 +687,13 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
                 const int r = b / bp.tiles_x;
                 const int tile = owned_row_of(bp, r) * bp.tiles_x + (b - r * bp.tiles_x);
                 const u32 beg = off[tile], end = off[tile + 1];
-                const u32 start = beg + atomicAdd(&cur[tile], h) - epoch * (end - beg);
+                const u32 start = beg + atomicAdd(&cur[tile], h + over) - epoch * (end - beg);
                 const bool bad = start < beg || start + h > end;
                 hist[b] = bad ? end : start;   // (bad: every slot of this range fails slot < end)
                 hlim[b] = end;
-                if (bad) __hip_atomic_store(&wstat[WS_TAG], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // (loose ranges: an overflowing tile's cursor ends past its range, and k_vis
+                // runs that tile over every triangle; the batch's other tiles are exact)
+                if (bad && !loose) __hip_atomic_store(&wstat[WS_TAG], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -686,9 +716,9 @@ __global__ __launch_bounds__(256) void k_bin_warm(const BinParams bp, const u32*
                 } else {
                     const u32 beg = off[hrow + tx];
                     end = off[hrow + tx + 1];
-                    slot = beg + atomicAdd(&cur[hrow + tx], 1u) - epoch * (end - beg);
+                    slot = beg + atomicAdd(&cur[hrow + tx], 1u + over) - epoch * (end - beg);
                     if (slot < beg || slot >= end) {
-                        __hip_atomic_store(&wstat[WS_TAG], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (!loose) __hip_atomic_store(&wstat[WS_TAG], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         slot = end;
                     }
                 }
@@ -999,15 +1029,21 @@ constexpr int KS = TW + 1;        // padded row stride of the LDS tile keys
 // schedule's warm batches, k_bin_warm); otherwise only that tile's items run
 // over every triangle.  The first workgroup to see a failure (wstat[WS_REP]
 // exchanged for the batch's tag) reports it in host-mapped *hfail (reason 1 a
-// tile over its range, 2 token timeout, 3 a tile's count wrong; nr_settle
-// latches an error and drops the schedule).  wstat null: a cold batch
-// (plan[3] == 0 there: the batch does nothing, the host re-runs it).
+// tile over its range, 2 token timeout, 3 a tile's count wrong, 4 a tile over
+// its loose range; nr_settle latches an error and drops the schedule, or for
+// 4 stops binning that buffer loose).  wstat null: a cold batch (plan[3] == 0
+// there: the batch does nothing, the host re-runs it).
+// Loose batches (a changed transform, loose ranges off = off2): the cursors
+// start at 0 and hold the tile's pair count n, which only has to fit the
+// tile's range; the tile's items then slice its n pairs afresh (item k of
+// nsl: [k n / nsl, (k + 1) n / nsl)).
 struct WarmCheck {
     u32* wstat;
     const u32* cur;   // the set's cursors
-    const u32* off;   // the schedule's tile offsets
+    const u32* off;   // the schedule's tile offsets (loose: its loose ranges)
     u32 tag, mult;
     u32* hfail;
+    u32 loose;
 };
 
 // One report per failed warm batch (see WarmCheck): words 1..3 for the
@@ -1081,10 +1117,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
         bool fbt = fb;   // this tile's list is not trusted (WarmCheck)
         if (wc.wstat && !fb) {
             // (uniform values: scalar registers, nothing kept in VGPRs across the item)
-            const u32 cnt = __builtin_amdgcn_readfirstlane(wc.off[tile + 1] - wc.off[tile]);
+            const u32 beg = __builtin_amdgcn_readfirstlane(wc.off[tile]);
+            const u32 cnt = __builtin_amdgcn_readfirstlane(wc.off[tile + 1]) - beg;
             const u32 cu = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_load(&wc.cur[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            fbt = cu != wc.mult * cnt;
+            if (!wc.loose) {
+                fbt = cu != wc.mult * cnt;
+            } else {
+                fbt = cu > cnt;
+                if (!fbt) {   // this item's slice of the tile's cu pairs
+                    const u32 k = d.w >> 16;
+                    ls = beg + (u32)(((u64)k * cu) / nsl);
+                    le = beg + (u32)(((u64)(k + 1) * cu) / nsl);
+                }
+            }
             if (fbt) badTile = (u32)tile;   // (reported after the item loop: no report code live in it)
         }
         if (fbt) {   // this item's slice of all n triangles (never empty: a split tile has n >= its pairs > nsl)
@@ -1385,7 +1431,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
     if (tid == 0 && pr_item != ~0u) probe_item(pr_item, pr_d, pr_t0, __builtin_amdgcn_s_memrealtime(), NT);
 #endif
     if (badTile != ~0u && tid == 0)
-        warm_report(wc, 3u, badTile, wc.cur[badTile], wc.mult * (wc.off[badTile + 1] - wc.off[badTile]));
+        warm_report(wc, wc.loose ? 4u : 3u, badTile, wc.cur[badTile],
+                    (wc.loose ? 1u : wc.mult) * (wc.off[badTile + 1] - wc.off[badTile]));
     if (COUNT) {
         __syncthreads();
         atomicAdd(&sFrag, myFrags);
@@ -1424,7 +1471,8 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
                                   : (sc.lastN == 0 || sc.lastPairs > (u64)(COOP_PAIRS * (f64)sc.lastN));
     // wide workgroups when the last batch had few pairs (a sharded frame):
     // its dense items run at low occupancy and are latency-bound
-    const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < WIDE_HEAVY;
+    static const u32 wideHeavy = [] { const char* e = getenv("NR_WIDE_HEAVY"); return e ? (u32)atoi(e) : WIDE_HEAVY; }();
+    const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wideHeavy;
 #define NR_VIS(CO, NTT, ...)                                                                                       \
     hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, start, stop, 0, fp, va.items,    \
                           va.list, sc.kslot, sc.fdone, va.plan, wc)
@@ -1763,7 +1811,7 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
         nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = !e1;
         hipEvent_t st = vs ? F.evVis : e1;
-        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, nullptr, nullptr, 0u, 0u, nullptr}}, grid, sa, e0, st,
+        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, nullptr, nullptr, 0u, 0u, nullptr, 0u}}, grid, sa, e0, st,
                        zmode, g);
         NR_CHECK(hipGetLastError());
         nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
@@ -1849,6 +1897,34 @@ static bool sched_matches(const TriScratch& sc, const TriangleBuffer* tb, const 
            std::find(sc.warmBanned.begin(), sc.warmBanned.end(), tb->uid) == sc.warmBanned.end();
 }
 
+// Loose binning (round 6): the buffer of the schedule drawn under another
+// transform (same frame, shard pattern and depth mode), where no vertex moves
+// more than LOOSE_PX on screen from where the schedule's transform put it --
+// a moving or jittering scene.  Every tile's pair count then changes by the
+// triangles that cross its edges; the loose ranges (loose_cap) hold them, so
+// the batch bins in one pass (k_bin_warm) instead of count -> plan -> emit.
+// The displacement bound: the two affine maps differ by an affine map, whose
+// largest displacement over the buffer's bounding box is at one of its corners.
+constexpr f64 LOOSE_PX = 2.0;
+static bool loose_matches(const TriScratch& sc, const TriangleBuffer* tb, const BinKey& key) {
+    const auto& S = sc.sched;
+    if (!warm_on(sc) || !tb || !S.valid || S.tbUid != tb->uid || sc.capOverride) return false;
+    if (S.key.W != key.W || S.key.H != key.H || S.key.period != key.period || S.key.mask != key.mask) return false;
+    if (std::find(sc.warmBanned.begin(), sc.warmBanned.end(), tb->uid) != sc.warmBanned.end() ||
+        std::find(sc.looseBanned.begin(), sc.looseBanned.end(), tb->uid) != sc.looseBanned.end())
+        return false;
+    const f64* b = tb->bbox;
+    if (!(std::isfinite(b[0]) && std::isfinite(b[1]) && std::isfinite(b[2]) && std::isfinite(b[3]))) return false;
+    for (int c = 0; c < 4; ++c) {
+        const f64 x = b[(c & 1) ? 2 : 0], y = b[(c & 2) ? 3 : 1];
+        f64 ax, ay, bx, by;
+        nr_xform(S.key.m, x, y, ax, ay);
+        nr_xform(key.m, x, y, bx, by);
+        if (!(std::fabs(ax - bx) <= LOOSE_PX && std::fabs(ay - by) <= LOOSE_PX)) return false;
+    }
+    return true;
+}
+
 // A warm batch that failed its checks (k_vis WarmCheck: the raster then ran
 // over every triangle, so its frame is right) -- read at the next call into
 // the context: latch an error, drop the schedule (the next draw bins cold),
@@ -1862,9 +1938,17 @@ static void warm_poll(RenderContext* ctx) {
     const u32 w3 = __atomic_load_n(&sc.hfail[3], __ATOMIC_ACQUIRE);
     __atomic_store_n(sc.hfail, 0u, __ATOMIC_RELEASE);
     ++sc.warmFailures;
+    char msg[320];
+    if (f == 4) {   // a tile over its loose range: the schedule stays, the buffer is not binned loose again
+        if (sc.sched.valid) sc.looseBanned.push_back(sc.sched.tbUid);
+        snprintf(msg, sizeof msg, "triangle batch: a loose warm binning gave tile %u %u pairs, room for %u; that "
+                                  "tile was rasterised from all the batch's triangles and the buffer is no longer "
+                                  "binned loose", w1, w2, w3);
+        nr_set_error_msg(msg);
+        return;
+    }
     if (f != 2 && sc.sched.valid) sc.warmBanned.push_back(sc.sched.tbUid);
     sc.sched.valid = false;
-    char msg[320];
     if (f == 2)
         snprintf(msg, sizeof msg, "triangle batch: a raster's wait for its warm binning timed out; the batch was "
                                   "rasterised from all its triangles (under serialised kernel dispatch -- a "
@@ -1989,7 +2073,11 @@ static void warm_blocks(RenderContext* ctx, const BinParams& bp, const TriangleB
     S.blocksGen = S.gen;
 }
 
-static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinParams& bp, const TriangleBuffer* tb) {
+// loose: the batch's transform differs from the schedule's (loose_matches):
+// bin into the schedule's loose ranges, cursors from 0 (k_bin_warm), and let
+// k_vis slice each tile's actual count.
+static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinParams& bp, const TriangleBuffer* tb,
+                         bool loose = false) {
     const f64* tbCbox = tb->cbox;
     TriScratch& sc = ctx->tri;
     auto& S = sc.sched;
@@ -2008,7 +2096,11 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     }
     // cursors [0, ntiles), then the batch checks {report tag, error tag} (WarmCheck)
     const size_t tneed = std::max<size_t>((size_t)ntiles + 2, TILE_ARR);
-    const bool grow = F.ftile_cap < tneed || !F.fcnt || F.flist_cap < std::max<size_t>(S.pairs, 1) ||
+    if (loose && S.off2Gen != S.gen)   // (a bound of the loose list: every tile's loose_cap)
+        S.pairs2 = (u64)S.pairs + S.pairs / 4 + 64ull * (u64)(ntiles + 1);
+    const size_t lneed = std::max<size_t>(loose ? (size_t)S.pairs2 : (size_t)S.pairs, 1);
+    if (loose && lneed >= 0xF0000000ull) return false;
+    const bool grow = F.ftile_cap < tneed || !F.fcnt || F.flist_cap < lneed ||
                       sc.kslot_cap < std::max<size_t>(S.split, 1) * (TH * TW) || sc.fdone_cap < (size_t)ntiles + 1;
     if (grow) {   // (first use of a set, or a larger schedule: rare)
         NR_CHECK(hipStreamSynchronize(sa));
@@ -2022,7 +2114,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
             F.curGen = 0;
         }
         u32* lb[1] = {F.flist};
-        if (!grow_set(lb, &F.flist_cap, std::max<size_t>(S.pairs, 1))) return false;
+        if (!grow_set(lb, &F.flist_cap, lneed)) return false;
         F.flist = lb[0];
         u64* kb[1] = {sc.kslot};
         if (!grow_set(kb, &sc.kslot_cap, std::max<size_t>(S.split, 1) * (TH * TW))) return false;
@@ -2033,15 +2125,31 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
         sc.fdone = db[0];
         if (sc.fdone_cap != olddone) NR_CHECK(hipMemsetAsync(sc.fdone, 0, sc.fdone_cap * sizeof(u32), sa));
     }
-    if (tbCbox) warm_blocks(ctx, bp, tb);
+    // (the active blocks are found under the schedule's own transform: a loose batch launches them all)
+    if (tbCbox && !loose) warm_blocks(ctx, bp, tb);
+    if (loose && S.off2Gen != S.gen) {   // the schedule's loose ranges, once (main stream, before S.ready)
+        if (S.off2_cap < (size_t)ntiles + 1) {
+            NR_CHECK(hipStreamSynchronize(sa));
+            NR_CHECK(hipStreamSynchronize(nr_bin_stream_for(ctx->device)));
+            u32* ob[1] = {S.off2};
+            if (!grow_set(ob, &S.off2_cap, (size_t)ntiles + 1)) return false;
+            S.off2 = ob[0];
+        }
+        hipLaunchKernelGGL(k_loose_off, dim3(1), dim3(1024), 0, sa, (const u32*)S.off, S.off2, ntiles);
+        NR_CHECK(hipGetLastError());
+        NR_CHECK(hipEventRecord(S.ready, sa));
+        S.waitReady = true;
+        S.off2Gen = S.gen;
+    }
     if (F.visRecorded && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, F.evVis, 0));
     if (S.waitReady && sb != sa) NR_CHECK(hipStreamWaitEvent(sb, S.ready, 0));
     S.waitReady = false;
     // cursors: epoch e of this schedule on this set (k_bin_warm); zeroed for a
     // new schedule, after a cold batch on the set, or before they could wrap
-    if (F.curGen != S.gen || (u64)(F.curEpoch + 1) * std::max<u32>(S.pairs, 1) >= 0xF0000000ull) {
+    // (loose: from zero every batch -- they count the tile's pairs)
+    if (loose || F.curGen != S.gen || (u64)(F.curEpoch + 1) * std::max<u32>(S.pairs, 1) >= 0xF0000000ull) {
         NR_CHECK(hipMemsetAsync(F.fcur, 0, ((size_t)ntiles + 2) * sizeof(u32), sb));   // (and the check words)
-        F.curGen = S.gen;
+        F.curGen = loose ? 0 : S.gen;
         F.curEpoch = 0;
     }
     const int hbins = bp.hrows * fp.tiles_x;
@@ -2066,26 +2174,27 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     }
     const bool xs = sb != sa && !e1 && !gated;
     hipEvent_t binStop = xs ? F.evBin : nullptr;
-    const u32 epoch = F.curEpoch++;
+    const u32 epoch = loose ? 0u : F.curEpoch++;
     if (++sc.warmTag == 0) sc.warmTag = 1;
     const u32 tag = sc.warmTag;
     u32* const wstat = F.fcur + ntiles;   // {report tag, error tag} (WS_REP, WS_TAG)
     const int inject = sc.warmInject;
     sc.warmInject = 0;
     // cluster culling of the rank's tile rows, and only the schedule's active blocks launched
-    const f64* cbox = S.anyCull ? tbCbox : nullptr;
-    const bool useBlocks = cbox && S.blocksGen == S.gen;
+    const f64* cbox = S.anyCull || loose ? tbCbox : nullptr;
+    const bool useBlocks = cbox && !loose && S.blocksGen == S.gen;
+    const u32* const binOff = loose ? S.off2 : S.off;
     const u32* blocks = useBlocks ? S.blocks : nullptr;
     const int grid = useBlocks ? (int)S.nblocks : gb;
     if (inject == 4 && gated) hipLaunchKernelGGL(k_delay_binning, dim3(1), dim3(64), 0, sb);
     if (grid > 0) {
         if (ldsh)
             hipExtLaunchKernelGGL(k_bin_warm<true>, dim3(grid), dim3(256), (u32)(2 * hbins * sizeof(u32)), sb, nullptr,
-                                  binStop, 0, bp, (const u32*)S.off, F.fcur, F.flist, wstat, tag, epoch, cbox, blocks,
-                                  (u32)inject);
+                                  binStop, 0, bp, binOff, F.fcur, F.flist, wstat, tag, epoch, cbox, blocks, (u32)inject,
+                                  (u32)loose);
         else
-            hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(grid), dim3(256), 0, sb, nullptr, binStop, 0, bp,
-                                  (const u32*)S.off, F.fcur, F.flist, wstat, tag, epoch, cbox, blocks, (u32)inject);
+            hipExtLaunchKernelGGL(k_bin_warm<false>, dim3(grid), dim3(256), 0, sb, nullptr, binStop, 0, bp, binOff,
+                                  F.fcur, F.flist, wstat, tag, epoch, cbox, blocks, (u32)inject, (u32)loose);
     } else if (binStop) {
         NR_CHECK(hipEventRecord(F.evBin, sb));
     }
@@ -2112,7 +2221,7 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     if (S.nitems > 0) {
         nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
         const bool vs = !e1;
-        const WarmCheck wc{wstat, F.fcur, S.off, tag, epoch + 1, sc.dfail};
+        const WarmCheck wc{wstat, F.fcur, binOff, tag, epoch + 1, sc.dfail, (u32)loose};
         launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa, e0,
                        vs ? F.evVis : e1, zmode, fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
@@ -2176,6 +2285,16 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
             ++sc.warmBatches;
             finish_batch(ctx, fp);
         }
+        return;
+    }
+    if (getenv("NR_DEBUG_LOOSE"))
+        fprintf(stderr, "loose? valid=%d uid=%d lm=%d\n", (int)sc.sched.valid, (int)(tb && sc.sched.tbUid == tb->uid),
+                (int)loose_matches(sc, tb, key));
+    if (!ordered && !exact && loose_matches(sc, tb, key) && warm_enqueue(ctx, fp, bp, tb, true)) {
+        ctx->lastPath = 1;
+        ++sc.warmBatches;
+        ++sc.looseBatches;
+        finish_batch(ctx, fp);
         return;
     }
     const int si = sc.fnext;
@@ -2272,9 +2391,15 @@ void settle(RenderContext* ctx) {
         NR_CHECK(hipEventSynchronize(F.evVis));
         u32 seq = 0;
         const bool sorted = pb->ordered && plan_val(F, 6) > ORD_SORT_CAP;
-        if (sorted || free_enqueue(ctx, pb->src, pb->fp, pb->bp, true, pb->set, false, &seq, 0, 0, false, 0, pb->ordered) ==
-                          ENQ_SORTED)
+        int rr = ENQ_SORTED;
+        if (sorted || (rr = free_enqueue(ctx, pb->src, pb->fp, pb->bp, true, pb->set, false, &seq, 0, 0, false, 0,
+                                         pb->ordered)) == ENQ_SORTED)
             rerun_ordered_sorted(ctx, pb->src, pb->fp, pb->bp);   // (the context's flags are left as they are now)
+        else if (rr == ENQ_OK && !pb->ordered) {   // the exact re-run's binning is the buffer's schedule under this key
+            record_known(pb->tb, pb->key, (u32)sc.lastPairs, sc.lastHeavy, sc.lastItems, sc.lastSplit);
+            sched_capture(ctx, F, pb->key, pb->tb, pb->fp.tiles_x * pb->fp.tiles_y, (u32)sc.lastPairs, sc.lastItems,
+                          sc.lastHeavy, sc.lastSplit, (u64)pb->src.n);
+        }
     }
     delete pb;
 }

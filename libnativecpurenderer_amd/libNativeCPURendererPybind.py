@@ -453,6 +453,11 @@ class RenderContext:
     def warm_batch_count(self) -> int:
         return lib.GetWarmBatchCount(self._ptr)
 
+    def loose_batch_count(self) -> int:
+        """Of the warm batches, those binned into the loose ranges of the
+        schedule (the same buffer under a transform moved by <= 2 px)."""
+        return lib.GetLooseBatchCount(self._ptr)
+
     def packed(self) -> "PackedCommands":
         """A packing front end of this context: its draw and state calls go
         to the library as one array per submit() (ExecuteCommands)."""

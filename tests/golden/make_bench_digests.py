@@ -14,8 +14,8 @@ sha256[:32] of the band's f64 rows, depth rows, u8 RGB rows and YUV420P rows
 (Y rows of the band, then its U rows, then its V rows).  Any rank share is
 checked as the digests of the bands it owns; a whole frame as all of them.
 
-c3_animated alternates its transform (translate 0.37 * (i % 2), 0): one entry
-per parity of the frame index.
+c3_animated translates by bench.anim_tx(i) in frame i: one entry per frame
+index in bench.ANIM_DIGEST_FRAMES.
 
     python tests/golden/make_bench_digests.py [config ...]
 """
@@ -51,8 +51,9 @@ def band_digests(b, f64, depth, u8, yuv, W, H):
             for kind, a in (("f64", f64), ("depth", depth), ("rgb", u8), ("yuv420p", yuv))}
 
 
-def oracle_frame(cfg, xy, z, c, parity=0):
-    """One bench frame on the oracle (bench.Runner.frame's calls)."""
+def oracle_frame(cfg, xy, z, c, tx=0.0):
+    """One bench frame on the oracle (bench.Runner.frame's calls; tx: the
+    animated workload's translate)."""
     import scenes
     ctx = scenes.OracleFactory().context(cfg["W"], cfg["H"], False)
     ctx.set_color(0, 0, 0, 0)
@@ -60,17 +61,13 @@ def oracle_frame(cfg, xy, z, c, parity=0):
     ctx.clear_depth()
     if cfg.get("animate"):
         ctx.save_state()
-        ctx.translate(0.37 * parity, 0.0)
+        ctx.translate(tx, 0.0)
         ctx.draw_triangles(xy, c, z=z)
         ctx.restore_state()
     else:
         ctx.draw_triangles(xy, c, z=z)
     u8 = ctx.get_buffer_as_uint8_numpy()
     return (ctx.get_buffer_numpy(), ctx.get_depth_buffer(), u8, scenes.yuv420p(u8), ctx.last_fragment_count())
-
-
-def entry_key(config, parity=0):
-    return config + (f"@{parity}" if config == "c3_animated" else "")
 
 
 def make(configs=None):
@@ -81,14 +78,15 @@ def make(configs=None):
     for name in configs or sorted(b.CONFIGS):
         cfg = b.CONFIGS[name]
         xy, z, c = b.make_scene(cfg)
-        for parity in ((0, 1) if cfg.get("animate") else (0,)):
+        for fi in (b.ANIM_DIGEST_FRAMES if cfg.get("animate") else (0,)):
             t0 = time.time()
-            f64, depth, u8, yuv, frags = oracle_frame(cfg, xy, z, c, parity)
+            f64, depth, u8, yuv, frags = oracle_frame(cfg, xy, z, c, b.anim_tx(fi) if cfg.get("animate") else 0.0)
             assert b.BAND_ROWS == BAND
             d = band_digests(b, f64, depth, u8, yuv, cfg["W"], cfg["H"])
-            data[entry_key(name, parity)] = {"W": cfg["W"], "H": cfg["H"], "band_rows": BAND,
-                                             "triangles": int(len(xy)), "fragments": int(frags), **d}
-            print(f"{entry_key(name, parity)}: {frags} fragments, {time.time() - t0:.1f} s", flush=True)
+            key = b.digest_key(name, cfg, fi)
+            data[key] = {"W": cfg["W"], "H": cfg["H"], "band_rows": BAND, "triangles": int(len(xy)),
+                         "fragments": int(frags), **d}
+            print(f"{key}: {frags} fragments, {time.time() - t0:.1f} s", flush=True)
     with open(OUT, "w") as f:
         json.dump(data, f, indent=0, sort_keys=True)
         f.write("\n")

@@ -42,9 +42,9 @@ def _bench():
 _ORACLE = {}
 
 
-def _oracle_frame(b, config, parity=0):
+def _oracle_frame(b, config, frame=0):
     """(f64, depth, u8) of one bench frame on the oracle (cached per config)."""
-    key = (config, parity)
+    key = (config, frame)
     if key not in _ORACLE:
         _ORACLE.clear()   # (one 4K frame held at a time: ~250 MB)
         cfg = b.CONFIGS[config]
@@ -55,7 +55,7 @@ def _oracle_frame(b, config, parity=0):
         ctx.clear_depth()
         if cfg.get("animate"):
             ctx.save_state()
-            ctx.translate(0.37 * parity, 0.0)
+            ctx.translate(b.anim_tx(frame), 0.0)
             ctx.draw_triangles(xy, c, z=z)
             ctx.restore_state()
         else:
@@ -90,8 +90,8 @@ def _yuv_rows(yuv, W, H, rows):
     return y[rows], u[crow], v[crow]
 
 
-def _check(b, run, config, nsh, parity=0):
-    f64, depth, u8, frags = _oracle_frame(b, config, parity)
+def _check(b, run, config, nsh):
+    f64, depth, u8, frags = _oracle_frame(b, config)
     ctx, W, H = run.ctx, run.W, run.H
     rows = _owned_rows(b, H, nsh)
     assert ctx.warm_failure_count() == 0
@@ -135,13 +135,15 @@ def test_bench_rgb_frame_output_matches_oracle(gpu):
 
 @pytest.mark.slow
 def test_bench_animated_frames_match_oracle(gpu):
-    """extra.c3_animated: a new transform every frame (cold binning each
-    frame); the last frame of each parity checked."""
+    """extra.c3_animated: a new sub-pixel translate every frame -- after the
+    first cold binning, the frames bin into its loose ranges (the transform
+    moves no vertex more than 2 px); the last frame of an 11- and a 12-frame
+    run checked."""
     b = _bench()
     for nframes in (FRAMES, FRAMES - 1):
         run = _run_frames(b, "c3_animated", 1, "yuv420p", nframes)
-        parity = (nframes - 1) % 2
-        f64, depth, u8, _ = _oracle_frame(b, "c3_animated", parity)
+        assert run.ctx.loose_batch_count() >= nframes - 3, run.ctx.loose_batch_count()
+        f64, depth, u8, _ = _oracle_frame(b, "c3_animated", nframes - 1)
         g = run.ctx.get_buffer_numpy()
         assert scenes.bits_equal(g, f64), scenes.first_mismatch(g, f64)
         assert np.array_equal(run.ctx.get_depth_buffer(), depth)

@@ -169,3 +169,84 @@ def test_fresh_gate_set_beside_a_busy_device(gpu, oracle):
     assert ctx.warm_failure_count() == 0
     assert ctx.warm_batch_count() >= 3
     busy.flush()
+
+
+def _moving_frames(fac, W, H, scene, moves, shard=None, inject=None):
+    """One frame per transform in `moves` ((tx, ty, deg) applied on top of
+    the identity), the buffer drawn again every frame (GPU: TriangleBuffer)."""
+    xy, z, c = scene
+    ctx = fac.context(W, H, False)
+    if fac.name == "gpu":
+        from libnativecpurenderer_amd import libNativeCPURendererPybind as R
+        ctx.set_warm_binning(1)
+        if shard is not None:
+            ctx.set_shard(*shard)
+        buf = R.TriangleBuffer(xy, c, z=z, gouraud=True)
+    outs, loose = [], []
+    for k, (tx, ty, deg) in enumerate(moves):
+        if inject is not None and fac.name == "gpu" and k == inject[0]:
+            ctx.set_warm_fault_injection(inject[1])
+        ctx.set_color(0.1, 0.2, 0.3, 0.1)
+        ctx.set_depth_state(True, True)
+        ctx.clear_depth()
+        ctx.save_state()
+        ctx.translate(tx, ty)
+        if deg:
+            ctx.rotate_degree(deg)
+        if fac.name == "gpu":
+            ctx.draw_triangle_buffer(buf)
+        else:
+            ctx.draw_triangles(xy, c, z=z)
+        ctx.restore_state()
+        outs.append({"f64": ctx.get_buffer_numpy(), "depth": ctx.get_depth_buffer()})
+        if fac.name == "gpu":
+            loose.append(ctx.loose_batch_count())
+    ctx.loose_counts = loose
+    return outs, ctx
+
+
+# sub-pixel and pixel jitter, a rotation of a few hundredths of a degree (within 2 px at 640x400), a jump past
+# 2 px (cold, a new schedule), then jitter around the new place
+MOVES = [(0, 0, 0), (0.37, 0, 0), (0.9, -0.6, 0), (-1.4, 1.9, 0), (0.2, 0.1, 0.05), (1.99, -1.99, 0),
+         (7.5, 3.0, 0), (7.9, 3.3, 0), (6.2, 2.0, 0), (0.0, 0.0, 0)]
+
+
+@pytest.mark.parametrize("shard", [None, (2, 1), (8, 3)])
+def test_loose_binning_of_a_moving_scene(gpu, oracle, shard):
+    """A TriangleBuffer drawn under a new transform every frame (round 6):
+    frames within 2 px of the last cold binning's transform bin into its
+    loose ranges (k_bin_warm, k_vis slicing each tile's actual count), a jump
+    beyond bins cold and becomes the new schedule.  Every frame equals the
+    oracle's, bit for bit."""
+    W, H = 640, 400
+    scene = _scene(W, H)
+    want, _ = _moving_frames(oracle, W, H, scene, MOVES)
+    got, ctx = _moving_frames(gpu, W, H, scene, MOVES, shard=shard)
+    rows = slice(None) if shard is None else _owned(H, *shard)
+    for k, (g, o) in enumerate(zip(got, want)):
+        assert scenes.bits_equal(g["f64"][rows], o["f64"][rows]), f"frame {k}: {scenes.first_mismatch(g['f64'][rows], o['f64'][rows])}"
+        assert np.array_equal(g["depth"][rows], o["depth"][rows]), f"frame {k} depth"
+    assert ctx.warm_failure_count() == 0
+    # loose: frames 1-3 (within 2 px of frame 0), 7 and 8 (of frame 6); the rotated frame moves the huge
+    # off-screen clusters by far more than 2 px, so frames 4-6 and 9 bin cold
+    assert ctx.loose_counts == [0, 1, 2, 3, 3, 3, 3, 4, 5, 5], ctx.loose_counts
+
+
+def test_loose_overflow_falls_back_exactly(gpu, oracle):
+    """A loose batch whose tiles run past their loose ranges (fault 1 under a
+    changed transform): those tiles are rasterised from every triangle (the
+    frame stays exact), the failure is latched, and the buffer is not binned
+    loose again (later moved frames bin cold, the exact repeat stays warm)."""
+    from libnativecpurenderer_amd import _lib
+    W, H = 640, 400
+    scene = _scene(W, H)
+    moves = [(0, 0, 0), (0.5, 0, 0), (0.25, 0.5, 0), (1.0, 1.0, 0), (0.5, 0.5, 0)]
+    want, _ = _moving_frames(oracle, W, H, scene, moves)
+    _lib.clear_error()
+    got, ctx = _moving_frames(gpu, W, H, scene, moves, inject=(2, 1))
+    for k, (g, o) in enumerate(zip(got, want)):
+        assert scenes.bits_equal(g["f64"], o["f64"]), f"frame {k}: {scenes.first_mismatch(g['f64'], o['f64'])}"
+        assert np.array_equal(g["depth"], o["depth"]), f"frame {k} depth"
+    assert ctx.warm_failure_count() == 1
+    assert "loose" in _lib.last_error(), _lib.last_error()
+    assert ctx.loose_batch_count() == 2   # frames 1 and 2; none after the failure
