@@ -103,9 +103,6 @@ def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True, frame_out="rgb"):
 # --warmup 5 --steps 20) would otherwise time part of the ramp (~3-6 %,
 # profiles/r04/warmup_steps20.txt).  Reported as "clock_settle" in the line.
 CLOCK_SETTLE_MS = 60.0
-EVENT_EVERY = 10   # timed-region frames per timed launch of the dominant kernel (--event-every): binding
-                   # the events to every launch costs ~10 us per C3 frame (0.1325-0.138 against 0.1225-0.1231 ms,
-                   # profiles/r06/ab_event_every.txt); every 10th costs nothing measurable
 
 KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)"}
 
@@ -467,27 +464,37 @@ class Runner:
         kb = kernel_bytes(self.cfg, self.n_tri, path, share, self.frame_output)
         dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
-        # (2) timed region: K frames.  The dominant kernel is timed by its own
-        #     dispatch timestamps (hipExtLaunchKernel start/stop events bound to
-        #     the launch: no marker packets on the stream, the kernel's execution
-        #     time as rocprofv3's kernel trace has it) on every --event-every-th frame
-        timing = not self.args.no_kernel_timing
-        ctx.reset_kernel_timing()
-        ctx.set_kernel_timing_filter("" if not timing else dom)
+        # (2) kernel pass: K frames with only the dominant kernel timed, by its
+        #     own dispatch timestamps (hipExtLaunchKernel start/stop events bound
+        #     to the launch: no marker packets on the stream; the kernel's
+        #     execution time, as rocprofv3's kernel trace reports it).  Binding
+        #     the events costs the stream ~10 us per frame (profiles/r06/
+        #     ab_event_every.txt), so the timed region below carries none.
+        dom_us, cnt = kernels[dom], 0
+        if not self.args.no_kernel_timing:
+            ctx.reset_kernel_timing()
+            ctx.set_kernel_timing_filter(dom)
+            ctx.enable_kernel_timing(True)
+            for i in range(steps):
+                self.frame(i)
+            self.drain()
+            ctx.enable_kernel_timing(False)
+            tot, cnt = ctx.get_kernel_timing(dom)
+            if cnt:
+                dom_us = round(tot / cnt * 1e3, 2)
+            ctx.reset_kernel_timing()
+
+        # (3) timed region: K frames, nothing but the frames
         self.sync()
         warm0, loose0 = ctx.warm_batch_count(), ctx.loose_batch_count()
         t0 = time.perf_counter()
         for i in range(steps):
-            # (sampled mid-period: frame 0 follows the host sync before the timed region, its binning
-            # and raster not yet overlapped as in the steady state)
-            ctx.enable_kernel_timing(timing and i % self.args.event_every == self.args.event_every // 2)
             self.frame(i)
         self.drain()
         torch.cuda.synchronize()
         dt = self.max_over_ranks(time.perf_counter() - t0)
         if dist is not None:
             dist.barrier()
-        ctx.enable_kernel_timing(False)
         warm_frames = ctx.warm_batch_count() - warm0
         loose_frames = ctx.loose_batch_count() - loose0
         ms = dt / steps * 1e3
@@ -497,8 +504,6 @@ class Runner:
             if self.max_over_ranks(1.0 if ver["verified"] is False else 0.0) > 0:
                 ver["verified"] = False
             ver["warm_failures"] = int(self.max_over_ranks(float(ver["warm_failures"])))
-        tot, cnt = ctx.get_kernel_timing(dom)
-        dom_us = round(tot / cnt * 1e3, 2) if cnt else kernels[dom]
         achieved = kb[dom] / (dom_us * 1e-6) / 1e9
         B = algorithmic_bytes(self.cfg, self.n_tri, frame_out=self.frame_output)   # whole frame
         ksym = "k_tile_raster" if path == "ordered" else "k_vis"
@@ -510,8 +515,8 @@ class Runner:
                 # the bytes the kernel physically moved (PMC) over the same kernel time
                 "traffic_frac": round(traffic / (dom_us * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4) if traffic else None,
                 "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
-                "kernel_us_source": (f"dispatch timestamps of every {self.args.event_every}th timed launch "
-                                     f"({cnt} launches)" if cnt else "breakdown pass"),
+                "kernel_us_source": (f"dispatch timestamps of {cnt} launches (kernel pass of K frames before the "
+                                     f"timed region)" if cnt else "breakdown pass"),
                 "algorithmic_bytes_per_launch": kb[dom], "rank_share_of_frame": round(share, 6),
                 **frame_roofline(B, share, ms, self.world)}
         out = {
@@ -563,8 +568,6 @@ def parse_args(argv=None):
                          "bands: every rank copies its own bands straight into one shared pinned host frame "
                          "(DeliverFrameBands, no GPU gather: each GPU's PCIe link carries its share)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="time without per-kernel HIP events")
-    ap.add_argument("--event-every", type=int, default=EVENT_EVERY,
-                    help="time the dominant kernel's launch (its dispatch timestamps) on every k-th timed frame")
     ap.add_argument("--force-ordered", action="store_true", help="A/B: always take the in-order tile raster")
     ap.add_argument("--lib", default=None,
                     help="experiment: load another build of the library (tools/exp A/B and probe builds)")
@@ -691,7 +694,8 @@ def main():
         **{k: res[k] for k in VERIFY_KEYS if k in res},
         "kernel_us_note": "kernel_us: per-launch averages from a breakdown pass with events around every kernel "
                           "(the rasters by their dispatch timestamps); roofline.kernel_us: the dominant kernel's "
-                          "dispatch timestamps over the timed region (roofline.kernel_us_source)",
+                          "dispatch timestamps over a K-frame pass of its own (roofline.kernel_us_source); the "
+                          "timed region carries no events",
     }
     if "valu_roofline" in res:
         result["valu_roofline"] = res["valu_roofline"]

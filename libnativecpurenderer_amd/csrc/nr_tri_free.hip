@@ -1450,7 +1450,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
 // instance, which left the next batch's binning a slot beside the raster, was
 // dropped in round 5: 4 waves measured faster once k_vis was spill-free, C3
 // 0.147 -> 0.140 ms, profiles/r04/ab_instances.txt.)
-constexpr u32 WIDE_HEAVY = 512;
+// Round 6 re-measure (profiles/r06/ab_wide_heavy.txt): with ~226 dense tiles (C3
+// 8-way share) wide is 24 % faster; with ~444 (4-way share) and ~478 (1M
+// triangles at 1080p) the narrow one is 7 % faster, so the threshold moved
+// from 512 to 320.
+constexpr u32 WIDE_HEAVY = 320;
 
 // The k_vis inputs of one batch: its work items, pair list and plan totals
 // (a binning set's, or the warm schedule's).
@@ -1471,8 +1475,7 @@ void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, 
                                   : (sc.lastN == 0 || sc.lastPairs > (u64)(COOP_PAIRS * (f64)sc.lastN));
     // wide workgroups when the last batch had few pairs (a sharded frame):
     // its dense items run at low occupancy and are latency-bound
-    static const u32 wideHeavy = [] { const char* e = getenv("NR_WIDE_HEAVY"); return e ? (u32)atoi(e) : WIDE_HEAVY; }();
-    const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < wideHeavy;
+    const bool wide = !C && sc.lastN != 0 && sc.lastHeavy > 0 && sc.lastHeavy < WIDE_HEAVY;
 #define NR_VIS(CO, NTT, ...)                                                                                       \
     hipExtLaunchKernelGGL((k_vis<Z, __VA_ARGS__>), dim3(grid), dim3(NTT), 0, s, start, stop, 0, fp, va.items,    \
                           va.list, sc.kslot, sc.fdone, va.plan, wc)
@@ -2287,9 +2290,6 @@ void draw_free(RenderContext* ctx, const TriSrc& src, TriangleBuffer* tb, bool c
         }
         return;
     }
-    if (getenv("NR_DEBUG_LOOSE"))
-        fprintf(stderr, "loose? valid=%d uid=%d lm=%d\n", (int)sc.sched.valid, (int)(tb && sc.sched.tbUid == tb->uid),
-                (int)loose_matches(sc, tb, key));
     if (!ordered && !exact && loose_matches(sc, tb, key) && warm_enqueue(ctx, fp, bp, tb, true)) {
         ctx->lastPath = 1;
         ++sc.warmBatches;
