@@ -464,12 +464,12 @@ class Runner:
         kb = kernel_bytes(self.cfg, self.n_tri, path, share, self.frame_output)
         dom = max((k for k in kb if k in kernels), key=lambda k: kernels[k])
 
-        # (2) kernel pass: K frames with only the dominant kernel timed, by its
-        #     own dispatch timestamps (hipExtLaunchKernel start/stop events bound
-        #     to the launch: no marker packets on the stream; the kernel's
-        #     execution time, as rocprofv3's kernel trace reports it).  Binding
-        #     the events costs the stream ~10 us per frame (profiles/r06/
-        #     ab_event_every.txt), so the timed region below carries none.
+        # (2) kernel pass: K frames with only the dominant kernel timed: the
+        #     raster stamps its own execution span on the device's 100 MHz
+        #     clock (first workgroups' start, last workgroup's end; no packet
+        #     on the stream -- events around or bound to the launch also
+        #     counted the launch gap, profiles/r06/ab_event_every.txt).  The
+        #     timed region below carries no timing at all.
         dom_us, cnt = kernels[dom], 0
         if not self.args.no_kernel_timing:
             ctx.reset_kernel_timing()
@@ -515,8 +515,8 @@ class Runner:
                 # the bytes the kernel physically moved (PMC) over the same kernel time
                 "traffic_frac": round(traffic / (dom_us * 1e-6) / 1e9 / PEAK_HBM_GBPS, 4) if traffic else None,
                 "kernel": KERNEL_SYMBOL[dom], "kernel_us": dom_us,
-                "kernel_us_source": (f"dispatch timestamps of {cnt} launches (kernel pass of K frames before the "
-                                     f"timed region)" if cnt else "breakdown pass"),
+                "kernel_us_source": (f"device-clock span (s_memrealtime) of {cnt} launches, a K-frame pass before "
+                                     f"the timed region" if cnt else "breakdown pass"),
                 "algorithmic_bytes_per_launch": kb[dom], "rank_share_of_frame": round(share, 6),
                 **frame_roofline(B, share, ms, self.world)}
         out = {
@@ -693,9 +693,9 @@ def main():
         "clock_settle": res["clock_settle"],
         **{k: res[k] for k in VERIFY_KEYS if k in res},
         "kernel_us_note": "kernel_us: per-launch averages from a breakdown pass with events around every kernel "
-                          "(the rasters by their dispatch timestamps); roofline.kernel_us: the dominant kernel's "
-                          "dispatch timestamps over a K-frame pass of its own (roofline.kernel_us_source); the "
-                          "timed region carries no events",
+                          "(the rasters by their device-clock span); roofline.kernel_us: the dominant kernel's "
+                          "device-clock span over a K-frame pass of its own (roofline.kernel_us_source); the "
+                          "timed region carries no timing",
     }
     if "valu_roofline" in res:
         result["valu_roofline"] = res["valu_roofline"]

@@ -283,20 +283,24 @@ void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b) {
     nr_timing_end_on(ctx, kid, a, b, ctx->stream);
 }
 
-void nr_timing_kernel(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b) {
-    *a = *b = nullptr;
-    if (!ctx->timing || !((ctx->timingMask >> kid) & 1ull)) return;
-    *a = ev_get(ctx);
-    *b = ev_get(ctx);
-}
-void nr_timing_kernel_done(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b) {
-    if (!a) return;
-    ctx->evPending.push_back({kid, {a, b}});
-}
 
+constexpr int TS_PAIRS = 4096;   // timed raster launches between two collections
 static void timing_collect(RenderContext* ctx) {
-    if (ctx->evPending.empty()) return;
+    if (ctx->evPending.empty() && ctx->tsPending.empty()) return;
     NR_CHECK(hipStreamSynchronize(ctx->stream));
+    if (!ctx->tsPending.empty()) {   // device-clock pairs: ~start (max of inverted), end; 100 MHz
+        std::vector<u64> h(ctx->tsPending.size() * 2);
+        NR_CHECK(hipMemcpy(h.data(), ctx->tsDev, h.size() * sizeof(u64), hipMemcpyDeviceToHost));
+        for (auto& p : ctx->tsPending) {
+            const u64 s = ~h[2 * p.second], e = h[2 * p.second + 1];
+            if (!h[2 * p.second] || e < s) continue;   // (a launch that did no work)
+            ctx->kTimeMs[p.first] += (f64)(e - s) * 1e-5;
+            ctx->kCount[p.first] += 1;
+        }
+        NR_CHECK(hipMemsetAsync(ctx->tsDev, 0, h.size() * sizeof(u64), ctx->stream));
+        NR_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->tsPending.clear();
+    }
     for (auto& p : ctx->evPending) {
         float ms = 0;
         NR_CHECK(hipEventElapsedTime(&ms, p.second.first, p.second.second));
@@ -307,6 +311,19 @@ static void timing_collect(RenderContext* ctx) {
     }
     ctx->evPending.clear();
 }
+
+u64* nr_timing_stamp(RenderContext* ctx, int kid) {
+    if (!ctx->timing || !((ctx->timingMask >> kid) & 1ull)) return nullptr;
+    if ((int)ctx->tsPending.size() >= TS_PAIRS) timing_collect(ctx);
+    if (!ctx->tsDev) {
+        NR_CHECK(hipMalloc(&ctx->tsDev, (size_t)TS_PAIRS * 2 * sizeof(u64)));
+        NR_CHECK(hipMemsetAsync(ctx->tsDev, 0, (size_t)TS_PAIRS * 2 * sizeof(u64), ctx->stream));
+    }
+    const int i = (int)ctx->tsPending.size();
+    ctx->tsPending.push_back({kid, i});
+    return ctx->tsDev + 2 * i;
+}
+
 
 static const char* kKernelNames[NRK_COUNT_] = {"tri_count", "tri_scan",    "tri_emit", "tri_sort",
                                                "tile_ranges", "tile_raster", "prim",     "fill",
@@ -382,7 +399,7 @@ void DestroyRenderContext(RenderContext* ctx) {
     if (t.hfail) NR_CHECK(hipHostFree(t.hfail));
     {   // the warm-binning schedule
         auto& S = t.sched;
-        void* sp[] = {S.off, S.items, S.dplan, S.blocks};
+        void* sp[] = {S.off, S.items, S.dplan, S.blocks, S.off2};
         for (void* p : sp)
             if (p) NR_CHECK(hipFree(p));
         if (S.ready) NR_CHECK(hipEventDestroy(S.ready));
@@ -392,6 +409,7 @@ void DestroyRenderContext(RenderContext* ctx) {
         NR_CHECK(hipEventDestroy(p.second.second));
     }
     for (auto e : ctx->evPool) NR_CHECK(hipEventDestroy(e));
+    if (ctx->tsDev) NR_CHECK(hipFree(ctx->tsDev));
     delete ctx;
 }
 
@@ -784,7 +802,7 @@ void* GetStreamPtr(RenderContext* ctx) { return (void*)ctx->stream; }
 // frame inside a timed loop.
 void EnableKernelTiming(RenderContext* ctx, bool on) {
     ctx->timing = on;
-    if (ctx->evPending.size() >= 4096) timing_collect(ctx);
+    if (ctx->evPending.size() >= 4096 || ctx->tsPending.size() >= TS_PAIRS - 64) timing_collect(ctx);
 }
 
 // Sum and count of the named kernel's durations since the last reset

@@ -176,6 +176,8 @@ struct RenderContext {
     unsigned long long timingMask = ~0ull;   // which NRKernelId are timed
     std::vector<hipEvent_t> evPool;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> evPending;
+    u64* tsDev = nullptr;                    // device-clock stamp pairs of timed raster launches
+    std::vector<std::pair<int, int>> tsPending;   // (kernel id, pair index)
     f64 kTimeMs[NRK_COUNT_] = {0};
     i64 kCount[NRK_COUNT_] = {0};
     // covered-fragment counting (the work count of the Mpixels/s metric)
@@ -270,12 +272,11 @@ void nr_materialize_depth(RenderContext* ctx);
 void nr_materialize_tiles(RenderContext* ctx, bool color, bool depth);   // tile-granular pending clears
 void nr_ensure_depth(RenderContext* ctx);
 void nr_timing_begin(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
-// Timing of one kernel by its own dispatch timestamps: the pair is handed to
-// hipExtLaunchKernel as its start / stop events (no marker packets around the
-// kernel, so the stream is not perturbed and the time is the kernel's
-// execution, as rocprofv3's kernel trace reports it), then queued by _done.
-void nr_timing_kernel(RenderContext* ctx, int kid, hipEvent_t* a, hipEvent_t* b);
-void nr_timing_kernel_done(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);
+// The rasters time themselves on the device clock (FrameParams::tstamp,
+// raster_stamp_begin / _end): a zeroed {start, end} pair for one timed launch,
+// or null when not timed.  (Events bound to the launch, hipExtLaunchKernel
+// start/stop, measured the launch gap too: profiles/r06/ab_event_every.txt.)
+u64* nr_timing_stamp(RenderContext* ctx, int kid);
 void nr_timing_end(RenderContext* ctx, int kid, hipEvent_t a, hipEvent_t b);
 void nr_fill_f64(hipStream_t s, f64* p, i64 n, f64 v);
 void nr_fill_u32(hipStream_t s, u32* p, i64 n, u32 v);

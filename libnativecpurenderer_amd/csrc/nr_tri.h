@@ -353,7 +353,24 @@ struct FrameParams {
     int frameYUV;
     u32* tileStamp;   // non-null: k_vis leaves an empty tile's pending clears pending (stamps it tileEpoch,
     u32 tileEpoch;    // RenderContext::tileStamp) and writes only its frame output
+    u64* tstamp;      // non-null (kernel timing): {~first start, last end} of the raster on the device's
+                      // 100 MHz clock (raster_stamp_begin / _end, nr_timing_stamp)
 };
+
+// Kernel timing of the rasters by the device's constant 100 MHz clock
+// (s_memrealtime): the first workgroups dispatched on each XCD (blockIdx < 8)
+// max-in the inverted start time, every workgroup the end time -- the
+// kernel's execution span, as rocprofv3's kernel trace measures it, with no
+// packet on the stream (events around or bound to the launch add the launch
+// gap to the time; profiles/r06/ab_event_every.txt).
+__device__ __forceinline__ void raster_stamp_begin(const FrameParams& fp) {
+    if (fp.tstamp && threadIdx.x == 0 && blockIdx.x < 8)
+        atomicMax(reinterpret_cast<unsigned long long*>(&fp.tstamp[0]), ~__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void raster_stamp_end(const FrameParams& fp) {
+    if (fp.tstamp && threadIdx.x == 0)
+        atomicMax(reinterpret_cast<unsigned long long*>(&fp.tstamp[1]), __builtin_amdgcn_s_memrealtime());
+}
 
 // Frame output of pixel p = (px, py) from its framebuffer value, written by
 // the rasters' own write-back when they cover every owned pixel (a pending

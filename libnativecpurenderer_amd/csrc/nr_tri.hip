@@ -57,6 +57,7 @@ FrameParams frame_params(RenderContext* ctx, const TriSrc& src) {
     fp.frameYUV = ctx->frameFormat == 1;
     fp.tileStamp = nullptr;
     fp.tileEpoch = 0;
+    fp.tstamp = nullptr;
     if (ctx->countFragments) {
         if (!sc.d_frag) NR_CHECK(hipMalloc(&sc.d_frag, sizeof(u64)));
         NR_CHECK(hipMemsetAsync(sc.d_frag, 0, sizeof(u64), ctx->stream));

@@ -1076,6 +1076,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
     __shared__ u32 nU;
     __shared__ int sLast;
     __shared__ unsigned long long sFrag;
+    raster_stamp_begin(fp);
     bool fb = false;   // fallback: every triangle of the batch against every tile (WarmCheck)
     if (wc.wstat) {
         const u32 wt = __hip_atomic_load(&wc.wstat[WS_TAG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1430,6 +1431,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
 #if NR_PROBE
     if (tid == 0 && pr_item != ~0u) probe_item(pr_item, pr_d, pr_t0, __builtin_amdgcn_s_memrealtime(), NT);
 #endif
+    raster_stamp_end(fp);
     if (badTile != ~0u && tid == 0)
         warm_report(wc, wc.loose ? 4u : 3u, badTile, wc.cur[badTile],
                     (wc.loose ? 1u : wc.mult) * (wc.off[badTile + 1] - wc.off[badTile]));
@@ -1803,22 +1805,17 @@ static int free_enqueue(RenderContext* ctx, const TriSrc& src, const FrameParams
     }
 
     bool visDone = false;
+    FrameParams fpt = fp;   // (timed: the raster stamps itself on the device clock)
+    fpt.tstamp = nr_timing_stamp(ctx, NRK_TILE_RASTER);
     if (ordered) {   // one workgroup per tile, its list sorted in LDS
-        nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
-        const bool vs = !e1;
-        launch_ordered_binned(fp, F.flist, F.foff, F.dplan, F.frec, ntiles, sa, e0, vs ? F.evVis : e1);
+        launch_ordered_binned(fpt, F.flist, F.foff, F.dplan, F.frec, ntiles, sa, nullptr, F.evVis);
         NR_CHECK(hipGetLastError());
-        nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
-        visDone = vs;
+        visDone = true;
     } else if (grid > 0) {
-        nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
-        const bool vs = !e1;
-        hipEvent_t st = vs ? F.evVis : e1;
-        launch_vis_any(fp, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, nullptr, nullptr, 0u, 0u, nullptr, 0u}}, grid, sa, e0, st,
-                       zmode, g);
+        launch_vis_any(fpt, sc, VisArgs{F.fitems, F.flist, F.dplan, WarmCheck{nullptr, nullptr, nullptr, 0u, 0u, nullptr, 0u}},
+                       grid, sa, nullptr, F.evVis, zmode, g);
         NR_CHECK(hipGetLastError());
-        nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
-        visDone = vs;
+        visDone = true;
     }
     if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
     F.visRecorded = true;
@@ -2222,14 +2219,13 @@ static bool warm_enqueue(RenderContext* ctx, const FrameParams& fp, const BinPar
     const int zmode = fp.depthTest ? (fp.depthWrite ? 1 : 2) : 0;
     bool visDone = false;
     if (S.nitems > 0) {
-        nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
-        const bool vs = !e1;
+        FrameParams fpt = fp;   // (timed: the raster stamps itself on the device clock)
+        fpt.tstamp = nr_timing_stamp(ctx, NRK_TILE_RASTER);
         const WarmCheck wc{wstat, F.fcur, binOff, tag, epoch + 1, sc.dfail, (u32)loose};
-        launch_vis_any(fp, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa, e0,
-                       vs ? F.evVis : e1, zmode, fp.src.gouraud != 0);
+        launch_vis_any(fpt, sc, VisArgs{S.items, F.flist, visPlan, wc}, std::min<u32>(S.nitems, 8192), sa, nullptr,
+                       F.evVis, zmode, fp.src.gouraud != 0);
         NR_CHECK(hipGetLastError());
-        nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
-        visDone = vs;
+        visDone = true;
     }
     if (!visDone) NR_CHECK(hipEventRecord(F.evVis, sa));
     F.visRecorded = true;

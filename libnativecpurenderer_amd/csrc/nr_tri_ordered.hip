@@ -136,6 +136,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const i64 x0 = (i64)tx * TW, y0 = (i64)ty * TH;
     // (wave: uniform, so the per-wave masks and addresses below stay scalar)
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    raster_stamp_begin(fp);
     if (BINNED && !plan[3]) return;
     if (!owned_row(ty, fp.period, fp.mask)) return;
     const u32 ls = tstart[tile], le = BINNED ? tstart[tile + 1] : tend[tile];
@@ -456,6 +457,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             store_frame_out(fp, py * fp.W + px, px, py, cr[r], cg[r], cb[r], RGBA ? ca[r] : 1.0);
         }
     }
+    raster_stamp_end(fp);
     if (COUNT) {
         atomicAdd(&fragSum, myFrags);
         __syncthreads();
@@ -643,11 +645,11 @@ void ordered_sorted_kernels(RenderContext* ctx, const TriSrc& src, const FramePa
         list = sc.vals[1];
     }
 
-    nr_timing_kernel(ctx, NRK_TILE_RASTER, &e0, &e1);
-    if (fp.fragCounter) launch_raster_c<true, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec, nullptr, e0, e1);
-    else launch_raster_c<false, false>(fp, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec, nullptr, e0, e1);
+    FrameParams fpt = fp;   // (timed: the raster stamps itself on the device clock)
+    fpt.tstamp = nr_timing_stamp(ctx, NRK_TILE_RASTER);
+    if (fp.fragCounter) launch_raster_c<true, false>(fpt, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
+    else launch_raster_c<false, false>(fpt, list, sc.tile_start, sc.tile_end, ntiles, s, sc.orec);
     NR_CHECK(hipGetLastError());
-    nr_timing_kernel_done(ctx, NRK_TILE_RASTER, e0, e1);
 }
 
 }  // namespace

@@ -167,6 +167,10 @@ def run(frames=30, oracle=True):
         res["oracle_note"] = "CPU oracle (oracle/oracle.c, 1 thread), the same frame's draws; no frame output"
         for mode, g in outs.items():
             res[f"{mode}_bit_exact_vs_oracle"] = bool(scenes.bits_equal(g, o))
+        res["verified"] = all(res[f"{mode}_bit_exact_vs_oracle"] for mode in outs)
+    else:
+        res["verified"] = None
+        res["verify_note"] = "the oracle check runs with the CPU baseline (--no-cpu-baseline skips both)"
     return res
 
 
