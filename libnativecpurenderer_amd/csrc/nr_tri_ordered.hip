@@ -141,17 +141,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (!owned_row(ty, fp.period, fp.mask)) return;
     const u32 ls = tstart[tile], le = BINNED ? tstart[tile + 1] : tend[tile];
     if (ls == le && !fp.pendColor && !(DEPTH && fp.pendDepth)) return;
-    __shared__ f64 S[S_NSLOT][CH];
+    __shared__ f64 S[2][S_NSLOT][CH];   // (two chunks: one set up while the other is blended)
     // the lane masks of a wave's RPW steps for triangle k (bit l: lane l's
     // pixel of that step is covered), formed by the span phase's 512 threads
     // in VALU: the blend loop only moves them into scalar registers and sets
     // exec (it is bound by scalar issue)
-    __shared__ __attribute__((aligned(16))) u64 SPM[CH][NWAVE][RPW];
+    __shared__ __attribute__((aligned(16))) u64 SPM[2][CH][NWAVE][RPW];
     // span-phase ballots, one per column window q: HITQ[q][w] byte g = which of
     // triangles 8w..8w+7 touch window q of the tile rows 4g..4g+3
-    __shared__ u64 HITQ[NQ][NWAVE];
-    __shared__ iu8 VALID[CH];
-    __shared__ iu8 ZPASS[CH];   // depth test known to pass on every covered pixel (see zpass_all)
+    __shared__ u64 HITQ[2][NQ][NWAVE];
+    __shared__ iu8 ZPASS[2][CH];   // depth test known to pass on every covered pixel (see zpass_all)
     __shared__ u32 zmin_w[NWAVE];
     __shared__ unsigned long long fragSum;
     if (COUNT && tid == 0) fragSum = 0;
@@ -199,56 +198,66 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         for (int w = 1; w < NWAVE; ++w) zTileMin = min(zTileMin, zmin_w[w]);
     }
 
-    for (u32 base = ls; base < le; base += CH) {
-        const int cnt = (le - base) < (u32)CH ? (int)(le - base) : CH;
-        // ---- (a) triangle setup, one thread per triangle: the record
-        // k_tri_count formed (zpass_bound) and the per-tile parts
-        if (tid < cnt) {
-            const i64 t = list[base + tid];
+    // Chunks are double-buffered (round 6): while the waves blend chunk c
+    // (buffer buf), one wave -- a different one each chunk -- sets chunk c + 1
+    // up into buffer buf ^ 1 before its own blend, and after one barrier every
+    // wave forms chunk c + 1's spans: two barriers per chunk instead of three,
+    // and the setup's dependent global loads no longer keep seven waves waiting.
+    //
+    // (a) triangle setup of the chunk at cb into buffer sb, one lane of the
+    // calling wave per triangle: the record k_tri_count formed (zpass_bound)
+    // and the per-tile parts.  Returns the lane's vote for the blend-only loop
+    // (a chunk of flat translucent triangles whose depth test is proven to pass,
+    // or off: C5's common case).
+    auto setup = [&](u32 cb, int sb) -> bool {
+        const int cnt = (le - cb) < (u32)CH ? (int)(le - cb) : CH;
+        bool blendOnly = !GOURAUD;
+        if (lane < cnt) {
+            const int k = lane;
+            const i64 t = list[cb + k];
             const double2* r = reinterpret_cast<const double2*>(rec + t * ORec);
             const double2 v0 = r[0], v1 = r[1], v2 = r[2], v3 = r[3], v4 = r[4];
             const f64 sx[3] = {v0.x, v1.x, v2.x}, sy[3] = {v0.y, v1.y, v2.y};
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
-            VALID[tid] = 1;   // (only valid triangles are listed)
-            S[S_X0][tid] = sx[0]; S[S_Y0][tid] = sy[0];
-            S[S_X1][tid] = sx[1]; S[S_Y1][tid] = sy[1];
-            S[S_X2][tid] = sx[2]; S[S_Y2][tid] = sy[2];
-            S[S_E1X][tid] = e1x; S[S_E1Y][tid] = e1y; S[S_E2X][tid] = e2x; S[S_E2Y][tid] = e2y;
-            S[S_INV][tid] = v4.y;
-            S[S_SL0][tid] = v3.x; S[S_SL1][tid] = v3.y; S[S_SL2][tid] = v4.x;
+            S[sb][S_X0][k] = sx[0]; S[sb][S_Y0][k] = sy[0];
+            S[sb][S_X1][k] = sx[1]; S[sb][S_Y1][k] = sy[1];
+            S[sb][S_X2][k] = sx[2]; S[sb][S_Y2][k] = sy[2];
+            S[sb][S_E1X][k] = e1x; S[sb][S_E1Y][k] = e1y; S[sb][S_E2X][k] = e2x; S[sb][S_E2Y][k] = e2y;
+            S[sb][S_INV][k] = v4.y;
+            S[sb][S_SL0][k] = v3.x; S[sb][S_SL1][k] = v3.y; S[sb][S_SL2][k] = v4.x;
+            bool zok = !DEPTH;
             if (DEPTH) {
                 const double2 v5 = r[5], v6 = r[6];
                 const f64 z0 = v5.x, z1 = v5.y, z2 = v6.x;
-                S[S_Z0][tid] = z0; S[S_DZ1][tid] = z1 - z0; S[S_DZ2][tid] = z2 - z0;
+                S[sb][S_Z0][k] = z0; S[sb][S_DZ1][k] = z1 - z0; S[sb][S_DZ2][k] = z2 - z0;
                 const u32 zb = (u32)((u64)__double_as_longlong(v6.y) >> 32);
-                ZPASS[tid] = !fp.depthWrite && zb < zTileMin;   // zpass_all
+                zok = !fp.depthWrite && zb < zTileMin;   // zpass_all
+                ZPASS[sb][k] = zok;
             }
             if (GOURAUD) {
                 const f64* c = fp.src.rgba + t * 12;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    S[S_C0 + k][tid] = c[k];
-                    S[S_D1 + k][tid] = c[4 + k] - c[k];
-                    S[S_D2 + k][tid] = c[8 + k] - c[k];
+                for (int j = 0; j < 4; ++j) {
+                    S[sb][S_C0 + j][k] = c[j];
+                    S[sb][S_D1 + j][k] = c[4 + j] - c[j];
+                    S[sb][S_D2 + j][k] = c[8 + j] - c[j];
                 }
             } else {
                 const f64* c = fp.src.rgba + t * 4;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) S[S_C0 + k][tid] = c[k];
+                for (int j = 0; j < 4; ++j) S[sb][S_C0 + j][k] = c[j];
                 const f64 fR = c[0] * ct0, fG = c[1] * ct1, fB = c[2] * ct2, fA = c[3] * ct3;
-                S[S_FR][tid] = fR; S[S_FG][tid] = fG; S[S_FB][tid] = fB; S[S_FA][tid] = fA;
-                S[S_OM][tid] = 1 - fA;
-                S[S_RA][tid] = fR * fA; S[S_GA][tid] = fG * fA; S[S_BA][tid] = fB * fA;
+                S[sb][S_FR][k] = fR; S[sb][S_FG][k] = fG; S[sb][S_FB][k] = fB; S[sb][S_FA][k] = fA;
+                S[sb][S_OM][k] = 1 - fA;
+                S[sb][S_RA][k] = fR * fA; S[sb][S_GA][k] = fG * fA; S[sb][S_BA][k] = fB * fA;
+                blendOnly = zok && fA != 1;
             }
         }
-        // a chunk of flat translucent triangles whose depth test is proven to
-        // pass (or off) takes the blend-only loop below (C5's common case)
-        bool blendOnly = !GOURAUD;
-        if (!GOURAUD && tid < cnt) {
-            const bool zok = !DEPTH || ZPASS[tid] || !VALID[tid];
-            blendOnly = zok && S[S_FA][tid] != 1;
-        }
-        const bool allBlend = __syncthreads_and(blendOnly ? 1 : 0) != 0;
+        return blendOnly;
+    };
+    // (b) exact coverage spans of the chunk at cb (buffer sb)
+    auto spans = [&](u32 cb, int sb) {
+        const int cnt = (le - cb) < (u32)CH ? (int)(le - cb) : CH;
         // ---- (b) exact coverage spans: thread = (triangle k, row group rg =
         // tile rows 4rg..4rg+3); wave w takes triangles 8w..8w+7, lane = rg * 8
         // + (k - 8w).  Its 4 rows are 4 / SR steps of the waves of band rg / SR
@@ -260,10 +269,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
             for (int qq = 0; qq < NQ; ++qq) touch[qq] = false;
             if (k < cnt) {
-                const bool ok = VALID[k];
-                const f64 sx[3] = {S[S_X0][k], S[S_X1][k], S[S_X2][k]};
-                const f64 sy[3] = {S[S_Y0][k], S[S_Y1][k], S[S_Y2][k]};
-                const f64 sl[3] = {S[S_SL0][k], S[S_SL1][k], S[S_SL2][k]};
+                const bool ok = true;   // (only valid triangles are listed)
+                const f64 sx[3] = {S[sb][S_X0][k], S[sb][S_X1][k], S[sb][S_X2][k]};
+                const f64 sy[3] = {S[sb][S_Y0][k], S[sb][S_Y1][k], S[sb][S_Y2][k]};
+                const f64 sl[3] = {S[sb][S_SL0][k], S[sb][S_SL1][k], S[sb][S_SL2][k]};
                 // rows with a straddling edge: ymin <= y < ymax, where exactly
                 // two edges straddle (row_span_slopes = row_span there); none
                 // elsewhere (row_span's empty span)
@@ -292,23 +301,25 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 for (int j = 0; j < 4 / SR; ++j)
 #pragma unroll
                     for (int qq = 0; qq < NQ; ++qq) {
-                        SPM[k][b * NQ + qq][st0 + j] = mk[j * NQ + qq];
+                        SPM[sb][k][b * NQ + qq][st0 + j] = mk[j * NQ + qq];
                         touch[qq] |= mk[j * NQ + qq] != 0;
                     }
             }
 #pragma unroll
             for (int qq = 0; qq < NQ; ++qq) {
                 const u64 hit = __ballot(touch[qq]);
-                if (lane == 0) HITQ[qq][wave] = hit;
+                if (lane == 0) HITQ[sb][qq][wave] = hit;
             }
         }
-        __syncthreads();
+    };
+    // (c) in-order raster of the chunk in buffer sb
+    auto blend = [&](int sb, bool allBlend) {
         // this wave's triangles of the chunk (bit k: triangle k touches its
         // block): the bytes of its band's SR row groups in its window's ballots
         u64 hm = 0;
 #pragma unroll
         for (int w = 0; w < NWAVE; ++w) {
-            const u64 h = uniform_u64(HITQ[q][w]) >> (8 * band * SR);
+            const u64 h = uniform_u64(HITQ[sb][q][w]) >> (8 * band * SR);
             u64 m = 0;
 #pragma unroll
             for (int i = 0; i < SR; ++i) m |= h >> (8 * i);
@@ -327,11 +338,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             // this wave's block
             for (; hm; hm &= hm - 1) {
                 const int k = (int)__builtin_ctzll(hm);
-                const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
-                const f64 fA = RGBA ? S[S_FA][k] : 0.0;
+                const f64 om = S[sb][S_OM][k], RA = S[sb][S_RA][k], GA = S[sb][S_GA][k], BA = S[sb][S_BA][k];
+                const f64 fA = RGBA ? S[sb][S_FA][k] : 0.0;
                 u64 lm[RPW];
-                const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
-                const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
+                const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[sb][k][wave][0]);
+                const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[sb][k][wave][2]);
                 lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
                 lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
 #pragma unroll
@@ -344,27 +355,26 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     }
                 }
             }
-            __syncthreads();
-            continue;
+            return;
         }
         const f64 X = (f64)px;
         for (; hm; hm &= hm - 1) {
             const int k = (int)__builtin_ctzll(hm);
             u64 lm[RPW];
             {
-                const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][0]);
-                const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[k][wave][2]);
+                const ulonglong2 m01 = *reinterpret_cast<const ulonglong2*>(&SPM[sb][k][wave][0]);
+                const ulonglong2 m23 = *reinterpret_cast<const ulonglong2*>(&SPM[sb][k][wave][2]);
                 lm[0] = uniform_u64(m01.x); lm[1] = uniform_u64(m01.y);
                 lm[2] = uniform_u64(m23.x); lm[3] = uniform_u64(m23.y);
             }
             // (uniform: read into scalar registers, so the branches below are scalar)
-            const bool ztest = DEPTH && !__builtin_amdgcn_readfirstlane((int)ZPASS[k]);   // the depth expression is needed
+            const bool ztest = DEPTH && !__builtin_amdgcn_readfirstlane((int)ZPASS[sb][k]);   // the depth expression is needed
             if (!GOURAUD && !ztest) {
                 // flat colour, no per-pixel depth: ApplyPixel from the
                 // per-triangle terms on the covered lanes of each step
-                const f64 fA = __longlong_as_double((long long)uniform_u64((u64)__double_as_longlong(S[S_FA][k])));
+                const f64 fA = __longlong_as_double((long long)uniform_u64((u64)__double_as_longlong(S[sb][S_FA][k])));
                 if (fA != 1) {
-                    const f64 om = S[S_OM][k], RA = S[S_RA][k], GA = S[S_GA][k], BA = S[S_BA][k];
+                    const f64 om = S[sb][S_OM][k], RA = S[sb][S_RA][k], GA = S[sb][S_GA][k], BA = S[sb][S_BA][k];
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
                         if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
@@ -375,7 +385,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         }
                     }
                 } else {
-                    const f64 fR = S[S_FR][k], fG = S[S_FG][k], fB = S[S_FB][k];
+                    const f64 fR = S[sb][S_FR][k], fG = S[sb][S_FG][k], fB = S[sb][S_FB][k];
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
                         if (__builtin_amdgcn_inverse_ballot_w64(lm[r])) {
@@ -386,9 +396,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 }
                 continue;
             }
-            const f64 sx0 = S[S_X0][k], sy0 = S[S_Y0][k];
-            const f64 e1x = S[S_E1X][k], e1y = S[S_E1Y][k], e2x = S[S_E2X][k], e2y = S[S_E2Y][k];
-            const f64 inv = S[S_INV][k];
+            const f64 sx0 = S[sb][S_X0][k], sy0 = S[sb][S_Y0][k];
+            const f64 e1x = S[sb][S_E1X][k], e1y = S[sb][S_E1Y][k], e2x = S[sb][S_E2X][k], e2y = S[sb][S_E2Y][k];
+            const f64 inv = S[sb][S_INV][k];
             f64 pa = 0, pb = 0;   // dx * e2y, dx * e1y of this lane's column
             if (ztest || GOURAUD) {
                 const f64 dx = X - sx0;
@@ -397,9 +407,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             }
             f64 fR = 0, fG = 0, fB = 0, fA = 1, om = 0, RA = 0, GA = 0, BA = 0;
             if (!GOURAUD) {   // ApplyPixel's per-triangle terms (cpp:529-535), formed at setup
-                fR = S[S_FR][k]; fG = S[S_FG][k]; fB = S[S_FB][k]; fA = S[S_FA][k];
-                om = S[S_OM][k];
-                RA = S[S_RA][k]; GA = S[S_GA][k]; BA = S[S_BA][k];
+                fR = S[sb][S_FR][k]; fG = S[sb][S_FG][k]; fB = S[sb][S_FB][k]; fA = S[sb][S_FA][k];
+                om = S[sb][S_OM][k];
+                RA = S[sb][S_RA][k]; GA = S[sb][S_GA][k]; BA = S[sb][S_BA][k];
             }
 #pragma unroll
             for (int r = 0; r < RPW; ++r) {
@@ -412,15 +422,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 }
                 u32 zq = 0;
                 if (ztest) {
-                    const f64 zz = S[S_Z0][k] + S[S_DZ1][k] * w1 + S[S_DZ2][k] * w2;
+                    const f64 zz = S[sb][S_Z0][k] + S[sb][S_DZ1][k] * w1 + S[sb][S_DZ2][k] * w2;
                     zq = nr_quantize_depth_hw(zz);
                     if (!(zq < cz[r])) continue;
                 }
                 if (GOURAUD) {
-                    f64 R = S[S_C0 + 0][k] + S[S_D1 + 0][k] * w1 + S[S_D2 + 0][k] * w2;
-                    f64 G = S[S_C0 + 1][k] + S[S_D1 + 1][k] * w1 + S[S_D2 + 1][k] * w2;
-                    f64 B = S[S_C0 + 2][k] + S[S_D1 + 2][k] * w1 + S[S_D2 + 2][k] * w2;
-                    f64 A = S[S_C0 + 3][k] + S[S_D1 + 3][k] * w1 + S[S_D2 + 3][k] * w2;
+                    f64 R = S[sb][S_C0 + 0][k] + S[sb][S_D1 + 0][k] * w1 + S[sb][S_D2 + 0][k] * w2;
+                    f64 G = S[sb][S_C0 + 1][k] + S[sb][S_D1 + 1][k] * w1 + S[sb][S_D2 + 1][k] * w2;
+                    f64 B = S[sb][S_C0 + 2][k] + S[sb][S_D1 + 2][k] * w1 + S[sb][S_D2 + 2][k] * w2;
+                    f64 A = S[sb][S_C0 + 3][k] + S[sb][S_D1 + 3][k] * w1 + S[sb][S_D2 + 3][k] * w2;
                     // ApplyPixel (cpp:529-547) on the register-resident pixel
                     R *= ct0; G *= ct1; B *= ct2; A *= ct3;
                     if (A != 1) {
@@ -441,6 +451,27 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 }
                 if (DEPTH && fp.depthWrite) cz[r] = zq;
             }
+        }
+    };
+
+    int buf = 0;
+    bool allB = false;
+    if (ls < le) {   // the first chunk: set up by wave 0
+        const bool bo = wave == 0 ? setup(ls, 0) : !GOURAUD;
+        allB = __syncthreads_and(bo ? 1 : 0) != 0;
+        spans(ls, 0);
+        __syncthreads();
+    }
+    u32 ci = 0;
+    for (u32 base = ls; base < le; base += CH, buf ^= 1, ++ci) {
+        const u32 nb = base + CH;
+        const bool more = nb < le;
+        bool bo = !GOURAUD;
+        if (more && wave == (int)((ci + 1) & (NWAVE - 1))) bo = setup(nb, buf ^ 1);
+        blend(buf, allB);
+        if (more) {
+            allB = __syncthreads_and(bo ? 1 : 0) != 0;
+            spans(nb, buf ^ 1);
         }
         __syncthreads();
     }

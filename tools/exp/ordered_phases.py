@@ -60,8 +60,9 @@ def run():
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import bench
-    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     from libnativecpurenderer_amd import _lib
+    _lib.LIB_PATH = os.path.join(ROOT, "tools", "exp", "oph.so")   # (the phase-clock build)
+    from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     cfg = bench.CONFIGS[sys.argv[2] if len(sys.argv) > 2 else "c5"]
     xy, z, c = bench.make_scene(cfg)
     ctx = R.RenderContext(cfg["W"], cfg["H"], False)
