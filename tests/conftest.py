@@ -24,6 +24,11 @@ def gpu():
     """The HIP library through its Pybind mirror.  Fails (never skips) when no
     device is usable: the GPU tests must not pass on a fallback."""
     import scenes
+    # torch's HIP runtime first (the tests that hand the library torch tensors
+    # need torch's device view; with the library's runtime loaded first, torch
+    # found no device when such a test ran before any other torch use)
+    import torch
+    torch.cuda.init()
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
     if R.device_count() <= 0:
         pytest.fail("no HIP device visible: GPU tests need an MI355X")
