@@ -978,31 +978,52 @@ __device__ __forceinline__ void shade_tile(const FrameParams& fp, i64 x0, i64 y0
     }
 }
 
-// Maximum of a non-negative value over the wave (DPP row shifts and row
-// broadcasts as in wave_scan, then lane 63's value): VALU steps instead of a
-// chain of six cross-lane permutes through LDS.
-__device__ __forceinline__ int wave_max(int v) {
+// ---- flattened chunk raster (k_vis FLAT) -------------------------------
+// A wave's chunk (one triangle per lane) is rasterised in two flattened
+// stages: its (triangle, row) pairs are dealt out 64 at a time (lane = row
+// slot: the row's span), and each such window's covered pixels 64 at a time
+// (lane = fragment) -- no lane idles on a short row or span beside a long one.
+// The lanes fetch their triangle's and row's terms by lane permutes.
+
+__device__ __forceinline__ int wave_scan_max(int v) {   // inclusive max scan (values >= 0)
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));   // row_shr:1
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));   // row_shr:2
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));   // row_shr:4
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));   // row_shr:8
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
+    return v;
 }
 
-__device__ __forceinline__ f64 readlane_f64(f64 v, int lane) {
+__device__ __forceinline__ int bperm(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ u32 bperm(u32 v, int src) { return (u32)__builtin_amdgcn_ds_bpermute(src << 2, (int)v); }
+__device__ __forceinline__ float bperm(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+__device__ __forceinline__ f64 bperm(f64 v, int src) {
     const u64 b = __double_as_longlong(v);
-    const u32 lo = __builtin_amdgcn_readlane((u32)b, lane), hi = __builtin_amdgcn_readlane((u32)(b >> 32), lane);
+    const u32 lo = (u32)__builtin_amdgcn_ds_bpermute(src << 2, (int)(u32)b);
+    const u32 hi = (u32)__builtin_amdgcn_ds_bpermute(src << 2, (int)(u32)(b >> 32));
     return __longlong_as_double((long long)(((u64)hi << 32) | lo));
 }
 
-// A triangle whose bounding box covers at least BIG_PX pixels of the tile is
-// rasterised by the whole wave rather than by its own lane (96 measured 4-6 %
-// slower on C2).
-constexpr int BIG_PX = 32;
-static_assert(TH <= 64, "coop raster: one lane per tile row");
-constexpr f64 COOP_PAIRS = 2.0;
+// Owner of each slot of the window [wb, wb + 64) (slot wb + lane): the highest
+// lane o whose run [st_o, st_o + n_o) (n_o > 0; runs in lane order, back to
+// back) starts at or before it -- the runs that start in the window mark
+// their first slot in the wave's 64 LDS words, an inclusive max scan carries
+// each mark forward, and `carry` (the owner of slot wb - 1) fills the slots
+// before the window's first mark.  (One wave, in-order LDS: the clear, the
+// marks and the read need no barrier.)
+__device__ __forceinline__ int window_owner(u32* mk, int lane, u32 st, u32 n, u32 wb, int carry) {
+    __hip_atomic_store(&mk[lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (n && st - wb < 64u)
+        __hip_atomic_fetch_max(&mk[st - wb], (u32)lane + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const int v = (int)__hip_atomic_load(&mk[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return max(wave_scan_max(v), carry + 1) - 1;
+}
+
+static_assert(TH <= 32 && TW <= 64, "flattened raster: a fragment's row in 5 bits, its triangle lane in 6");
+constexpr f64 COOP_PAIRS = 2.0;   // tile pairs per triangle above which k_vis takes the flattened raster
 constexpr u32 HEAVY_PRIO = 512;   // work items of at least this many triangles run at raised wave priority
 constexpr int KS = TW + 1;        // padded row stride of the LDS tile keys
 
@@ -1015,8 +1036,11 @@ constexpr int KS = TW + 1;        // padded row stride of the LDS tile keys
 // then the lane walks the triangle's rows in this tile (exact span,
 // row_span_slopes) and their pixels (depth + LDS atomic on the packed key,
 // two pixels per step).  Then the workgroup shades the tile (shade_tile).
-// COOP: large triangles rasterised by the whole wave (coop pass); the host picks it from the previous batch's
-// pair density -- the variant without it keeps fewer registers live for sliver meshes.
+// FLAT: the chunk's rows and pixels are instead dealt out 64 per window
+// (flattened raster, above): for batches whose triangles cover many pixels of
+// a tile (C2 -17 %, profiles/r06/ab_flat.txt); for sliver meshes the permutes
+// cost more than the lane raster's idle lanes (C3 +29 %).  The host picks it
+// from the previous batch's pair density (COOP_PAIRS).
 // NT: workgroup size (VWG, or 2 * VWG for batches with few pairs, whose dense
 // items are latency-bound: more waves per item).
 // The checks of a warm batch (k_bin_warm).  Batch-wide: the tag word
@@ -1056,7 +1080,7 @@ __device__ __forceinline__ void warm_report(const WarmCheck& wc, u32 why, u32 a,
     __hip_atomic_store(&wc.hfail[0], why, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int ZMODE, bool COUNT, bool GOURAUD, bool COOP, int NT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
+template <int ZMODE, bool COUNT, bool GOURAUD, bool FLAT, int NT>   // ZMODE 0: no test, 1: LESS+write, 2: LESS no write
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) void k_vis(const FrameParams fp, const uint4* __restrict__ items,
                                              const u32* __restrict__ list,
                                              u64* __restrict__ kslot, u32* __restrict__ done,
@@ -1188,11 +1212,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
 
         // this wave's chunks: c = wave, wave + NW, ...  One lane per triangle,
         // its setup in registers; the lane walks the triangle's rows in this
-        // tile (exact span from the per-edge slopes) and their pixels.  A
-        // triangle covering many pixels of the tile is instead rasterised by
-        // the whole wave (lane = row for the spans, then lane = (row, column) over
-        // blocks of rows sized to the widest span).  A short slice is cut into NW chunks so that every
-        // wave gets a share.
+        // tile (exact span from the per-edge slopes) and their pixels -- or,
+        // FLAT, the chunk's rows and then their pixels are dealt out to the
+        // lanes 64 per window.  A short slice is cut into NW chunks so that
+        // every wave gets a share.
         const u32 ns = le - ls;
         const u32 cs = ns >= 64u * NWV ? 64u : (ns + NWV - 1) / NWV;
         const u32 nch = (ns + cs - 1) / cs;
@@ -1244,14 +1267,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
             const f64 den = e1x * e2y - e2x * e1y;
             int r0 = 0, r1 = 0;   // rows with a straddling edge: ymin <= y < ymax (exact)
-            bool big = false;
             if (lane < cnt && tri_finite(sx, sy) && den != 0) {
                 const f64 ymn = fmin(fmin(sy[0], sy[1]), sy[2]), ymx = fmax(fmax(sy[0], sy[1]), sy[2]);
                 r0 = (int)clampd(ceil(ymn) - (f64)y0, (f64)rlo, (f64)rcap);
                 r1 = (int)clampd(ceil(ymx) - (f64)y0, (f64)rlo, (f64)rcap);
-                const f64 xmn = fmin(fmin(sx[0], sx[1]), sx[2]), xmx = fmax(fmax(sx[0], sx[1]), sx[2]);
-                const f64 bw = fmin(xmx, (f64)x0 + wlim) - fmax(xmn, (f64)x0);   // bbox width in the tile
-                big = COOP && (f64)(r1 - r0) * bw >= (f64)BIG_PX;
             }
             edge_slopes(sx, sy, sl);
             const f64 inv = 1.0 / den;
@@ -1262,57 +1281,98 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
             // Flat batches keep the f64 spans (the f32 ones cost the flat
             // instances 8-24 B/lane of spills).
             constexpr bool SPAN32 = GOURAUD && ZMODE != 2 && !COUNT;
-            // the wave's large triangles first, one at a time, all lanes on each
-            // (the keys are an order-free min / max, so the order of the two
-            // passes is free; this one reads every lane's screen vertices, so
-            // they are dead before the lane raster below)
-            for (u64 bm = COOP ? __ballot(big && r0 < r1) : 0ull; bm; bm &= bm - 1) {
-                const int src = (int)__builtin_ctzll(bm);
-                f64 bx[3], by[3], bs[3];
+            if constexpr (FLAT) {
+                // rows: the chunk's (triangle, row) pairs, 64 per window
+                const u32 nr = r0 < r1 ? (u32)(r1 - r0) : 0u;
+                const u32 rin = wave_scan(nr, lane);
+                const u32 R = (u32)__builtin_amdgcn_readlane((int)rin, 63), rex = rin - nr;
+                const int r0x = r0 - (int)rex;   // (row of slot s: s + r0x of its triangle's lane)
+                Span32 S32;
+                if (SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);
+                u32* const mk = reinterpret_cast<u32*>(lds + ShadeStage<GOURAUD, HS>::HT) + wave * 64;
+                int rcar = -1;
+                for (u32 rb = 0; rb < R; rb += 64) {
+                    const int o = window_owner(mk, lane, rex, nr, rb, rcar);
+                    rcar = __builtin_amdgcn_readlane(o, 63);
+                    const u32 slot = rb + (u32)lane;
+                    const int r = (int)slot + bperm(r0x, o);
+                    const f64 y = (f64)(int)(y0 + r);
+                    // (every permute with all lanes active: a permute reads 0 from an inactive lane)
+                    Span32 S;
+                    f64 ox[3], oy[3], os[3];
+                    u32 oid = 0;
+                    if (SPAN32) {
+                        S.L = {bperm(S32.L.x, o), bperm(S32.L.yhi, o), bperm(S32.L.ylo, o), bperm(S32.L.s, o),
+                               bperm(S32.L.ce, o)};
+                        S.T = {bperm(S32.T.x, o), bperm(S32.T.yhi, o), bperm(S32.T.ylo, o), bperm(S32.T.s, o),
+                               bperm(S32.T.ce, o)};
+                        S.B = {bperm(S32.B.x, o), bperm(S32.B.yhi, o), bperm(S32.B.ylo, o), bperm(S32.B.s, o),
+                               bperm(S32.B.ce, o)};
+                        S.ymid = bperm(S32.ymid, o);
+                        oid = bperm((u32)id1, o);
+                    } else {
 #pragma unroll
-                for (int v = 0; v < 3; ++v) {
-                    bx[v] = readlane_f64(sx[v], src);
-                    by[v] = readlane_f64(sy[v], src);
-                    bs[v] = readlane_f64(sl[v], src);
-                }
-                const f64 bi = readlane_f64(inv, src), bz0 = readlane_f64(zz0, src);
-                const f64 bd1 = readlane_f64(dz1, src), bd2 = readlane_f64(dz2, src);
-                const u64 bid = ((u64)__builtin_amdgcn_readlane((u32)(id1 >> 32), src) << 32) |
-                                (u64)__builtin_amdgcn_readlane((u32)id1, src);
-                const int br0 = __builtin_amdgcn_readlane(r0, src), br1 = __builtin_amdgcn_readlane(r1, src);
-                const f64 b1x = bx[1] - bx[0], b1y = by[1] - by[0], b2x = bx[2] - bx[0], b2y = by[2] - by[0];
-                // spans: lane l -> row br0 + l (at most TH <= 64 rows)
-                int lxs = 0, lxe = 0;
-                if (br0 + lane < br1) row_span_slopes(bx, by, bs, (f64)(int)(y0 + br0 + lane), (f64)x0, (f64)wlim, lxs, lxe);
-                if (COUNT) myFrags += (unsigned long long)(lxe - lxs);
-                // pixels: blocks of R rows x C columns (C = the widest span
-                // rounded up to a power of two, R = 64 / C), lane -> (row, column)
-                const int wmax = wave_max(lxe - lxs);
-                const int lc = wmax <= 8 ? 3 : wmax <= 16 ? 4 : wmax <= 32 ? 5 : 6;
-                const int nrows = br1 - br0, R = 64 >> lc;
-                // each lane's span packed (xs | xe << 16); a block's spans are
-                // fetched (one lane permute) while the block before it is
-                // rasterised, so the permute latency is not on the loop's chain
-                const int pk = lxs | (lxe << 16);
-                int rl = lane >> lc;
-                int nx = __shfl(pk, rl & 63, 64);
-                for (int g = 0; g < nrows; g += R, rl += R) {
-                    const int cur = nx;
-                    if (g + R < nrows) nx = __shfl(pk, (rl + R) & 63, 64);
-                    const int xs = cur & 0xFFFF, xe = cur >> 16;
-                    const int lx = xs + (lane & ((1 << lc) - 1));
-                    if (rl >= nrows || lx >= xe) continue;
-                    const int r = br0 + rl;
-                    if (ZMODE == 0) {
-                        atomicMax(&key[r * KS + lx], bid);
-                        continue;
+                        for (int v = 0; v < 3; ++v) {
+                            ox[v] = bperm(sx[v], o); oy[v] = bperm(sy[v], o); os[v] = bperm(sl[v], o);
+                        }
                     }
-                    const f64 dy = (f64)(int)(y0 + r) - by[0];
-                    frag_key<ZMODE>(key, zin, r * KS + lx, (f64)(int)(x0 + lx), dy, bx[0], b1x, b1y, b2x, b2y, bi, bz0,
-                                    bd1, bd2, bid);
+                    int xs = 0, xe = 0;
+                    if (slot < R) {
+                        if (SPAN32) {
+                            if (!row_span32(S, r, y, (float)wlim, xs, xe)) {
+                                f64 qx[3], qy[3];
+                                tri_screen(fp.src, fp.m, (i64)oid - 1, qx, qy);
+                                row_span_in(qx, qy, y, (f64)x0, (f64)wlim, xs, xe);
+                            }
+                        } else {
+                            row_span_slopes(ox, oy, os, y, (f64)x0, (f64)wlim, xs, xe);
+                        }
+                    }
+                    if (COUNT) myFrags += (unsigned long long)(xe - xs);
+                    const u32 len = xe > xs ? (u32)(xe - xs) : 0u;
+                    // the row's depth terms (frag_depth's e2x * dy and e1x * dy)
+                    f64 t1 = 0.0, t2 = 0.0;
+                    if (ZMODE != 0) {
+                        const f64 dy = y - bperm(sy[0], o);
+                        t1 = bperm(e2x, o) * dy;
+                        t2 = bperm(e1x, o) * dy;
+                    }
+                    // fragments of the window's rows, 64 per step
+                    const u32 fin = wave_scan(len, lane);
+                    const u32 F = (u32)__builtin_amdgcn_readlane((int)fin, 63), fex = fin - len;
+                    const int pk = (xs - (int)fex) * 2048 + (r << 6) + o;   // x - f, row, triangle lane
+                    int fcar = -1;
+                    for (u32 fb = 0; fb < F; fb += 64) {
+                        const int q = window_owner(mk, lane, fex, len, fb, fcar);
+                        fcar = __builtin_amdgcn_readlane(q, 63);
+                        const int pq = bperm(pk, q);
+                        const int to = pq & 63, rr = (pq >> 6) & 31;
+                        const int xx = (int)(fb + (u32)lane) + (pq >> 11);
+                        const u32 fid = bperm((u32)id1, to);
+                        if (ZMODE == 0) {
+                            if (fb + (u32)lane < F) atomicMax(&key[rr * KS + xx], (u64)fid);
+                            continue;
+                        }
+                        const f64 T1 = bperm(t1, q), T2 = bperm(t2, q);
+                        const f64 ox0 = bperm(sx[0], to), oe1y = bperm(e1y, to), oe2y = bperm(e2y, to);
+                        const f64 oin = bperm(inv, to), oz0 = bperm(zz0, to), od1 = bperm(dz1, to), od2 = bperm(dz2, to);
+                        if (fb + (u32)lane < F) {
+                            // frag_depth with the row's products: the same operations on the same values
+                            const f64 X = (f64)(int)(x0 + xx);
+                            const f64 dx = X - ox0;
+                            const f64 w1 = (dx * oe2y - T1) * oin;
+                            const f64 w2 = (T2 - dx * oe1y) * oin;
+                            const f64 zz = oz0 + od1 * w1 + od2 * w2;
+                            const u32 zq = nr_quantize_depth_hw(zz);
+                            const int kp = rr * KS + xx;
+                            if (ZMODE == 1) atomicMin(&key[kp], ((u64)zq << 32) | fid);
+                            else if (zq < zin[kp]) atomicMax(&key[kp], (u64)fid);
+                        }
+                    }
                 }
+                continue;
             }
-            if (r0 < r1 && !big) {
+            if (r0 < r1) {
                 Span32 S32;
                 if (SPAN32) S32 = span32_setup(sx, sy, sl, (f64)x0, (f64)y0);
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
@@ -1471,8 +1531,8 @@ template <int Z, bool C, bool G>
 void launch_vis(const FrameParams& fp, const TriScratch& sc, const VisArgs& va, u32 grid, hipStream_t s,
                 hipEvent_t start, hipEvent_t stop) {
     const WarmCheck wc = va.wc;
-    // coop pass when the previous batch had more than COOP_PAIRS tiles per
-    // triangle (large triangles), or when there is no history
+    // the flattened raster when the previous batch had more than COOP_PAIRS
+    // tiles per triangle (large triangles), or when there is no history
     const bool coop = sc.coopMode ? sc.coopMode == 1
                                   : (sc.lastN == 0 || sc.lastPairs > (u64)(COOP_PAIRS * (f64)sc.lastN));
     // wide workgroups when the last batch had few pairs (a sharded frame):
