@@ -1022,7 +1022,7 @@ __device__ __forceinline__ int window_owner(u32* mk, int lane, u32 st, u32 n, u3
     return max(wave_scan_max(v), carry + 1) - 1;
 }
 
-static_assert(TH <= 32 && TW <= 64, "flattened raster: a fragment's row in 5 bits, its triangle lane in 6");
+static_assert(TH <= 64, "flattened raster: a fragment's row in 6 bits");
 constexpr f64 COOP_PAIRS = 2.0;   // tile pairs per triangle above which k_vis takes the flattened raster
 constexpr u32 HEAVY_PRIO = 512;   // work items of at least this many triangles run at raised wave priority
 constexpr int KS = TW + 1;        // padded row stride of the LDS tile keys
@@ -1248,10 +1248,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
                 pz[0] = qz[0]; pz[1] = qz[1]; pz[2] = qz[2];
             }
         };
-        prefetch(pt);
+        // (FLAT: the chunk's vertices are loaded at its start -- a flattened
+        // chunk runs long enough that its next one's loads would only hold
+        // registers through it)
+        if (!FLAT) prefetch(pt);
         for (u32 c = wave; c < nch; c += NWV) {
             const u32 base = ls + c * cs;
             const int cnt = (int)((le - base) < cs ? (le - base) : cs);
+            if (FLAT) prefetch(pt);
             const u32 t = pt;
             f64 sx[3], sy[3], sl[3];
 #pragma unroll
@@ -1262,7 +1266,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
             const f64 zz0 = hasZ ? pz[0] : 0.0;
             const f64 dz1 = hasZ ? pz[1] - pz[0] : 0.0, dz2 = hasZ ? pz[2] - pz[0] : 0.0;
             pt = ptn;
-            prefetch(pt);
+            if (!FLAT) prefetch(pt);
             ptn = list_at(c + 2 * NWV);
             const f64 e1x = sx[1] - sx[0], e1y = sy[1] - sy[0], e2x = sx[2] - sx[0], e2y = sy[2] - sy[0];
             const f64 den = e1x * e2y - e2x * e1y;
@@ -1330,39 +1334,44 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(VIS_WPE))) v
                     }
                     if (COUNT) myFrags += (unsigned long long)(xe - xs);
                     const u32 len = xe > xs ? (u32)(xe - xs) : 0u;
-                    // the row's depth terms (frag_depth's e2x * dy and e1x * dy)
-                    f64 t1 = 0.0, t2 = 0.0;
+                    // the row's depth terms (frag_depth's e2x * dy and e1x * dy) and its
+                    // triangle's, held by the row's lane: a fragment fetches all of its
+                    // terms from one lane (one permute round)
+                    f64 t1 = 0.0, t2 = 0.0, ox0 = 0.0, oe1y = 0.0, oe2y = 0.0, oin = 0.0, oz0 = 0.0, od1 = 0.0, od2 = 0.0;
+                    const u32 rid = bperm((u32)id1, o);
                     if (ZMODE != 0) {
                         const f64 dy = y - bperm(sy[0], o);
                         t1 = bperm(e2x, o) * dy;
                         t2 = bperm(e1x, o) * dy;
+                        ox0 = bperm(sx[0], o); oe1y = bperm(e1y, o); oe2y = bperm(e2y, o);
+                        oin = bperm(inv, o); oz0 = bperm(zz0, o); od1 = bperm(dz1, o); od2 = bperm(dz2, o);
                     }
                     // fragments of the window's rows, 64 per step
                     const u32 fin = wave_scan(len, lane);
                     const u32 F = (u32)__builtin_amdgcn_readlane((int)fin, 63), fex = fin - len;
-                    const int pk = (xs - (int)fex) * 2048 + (r << 6) + o;   // x - f, row, triangle lane
+                    const int pk = (xs - (int)fex) * 64 + r;   // x - f, row
                     int fcar = -1;
                     for (u32 fb = 0; fb < F; fb += 64) {
                         const int q = window_owner(mk, lane, fex, len, fb, fcar);
                         fcar = __builtin_amdgcn_readlane(q, 63);
                         const int pq = bperm(pk, q);
-                        const int to = pq & 63, rr = (pq >> 6) & 31;
-                        const int xx = (int)(fb + (u32)lane) + (pq >> 11);
-                        const u32 fid = bperm((u32)id1, to);
+                        const u32 fid = bperm(rid, q);
+                        const int rr = pq & 63;
+                        const int xx = (int)(fb + (u32)lane) + (pq >> 6);
                         if (ZMODE == 0) {
                             if (fb + (u32)lane < F) atomicMax(&key[rr * KS + xx], (u64)fid);
                             continue;
                         }
                         const f64 T1 = bperm(t1, q), T2 = bperm(t2, q);
-                        const f64 ox0 = bperm(sx[0], to), oe1y = bperm(e1y, to), oe2y = bperm(e2y, to);
-                        const f64 oin = bperm(inv, to), oz0 = bperm(zz0, to), od1 = bperm(dz1, to), od2 = bperm(dz2, to);
+                        const f64 qx0 = bperm(ox0, q), qe1y = bperm(oe1y, q), qe2y = bperm(oe2y, q);
+                        const f64 qin = bperm(oin, q), qz0 = bperm(oz0, q), qd1 = bperm(od1, q), qd2 = bperm(od2, q);
                         if (fb + (u32)lane < F) {
                             // frag_depth with the row's products: the same operations on the same values
                             const f64 X = (f64)(int)(x0 + xx);
-                            const f64 dx = X - ox0;
-                            const f64 w1 = (dx * oe2y - T1) * oin;
-                            const f64 w2 = (T2 - dx * oe1y) * oin;
-                            const f64 zz = oz0 + od1 * w1 + od2 * w2;
+                            const f64 dx = X - qx0;
+                            const f64 w1 = (dx * qe2y - T1) * qin;
+                            const f64 w2 = (T2 - dx * qe1y) * qin;
+                            const f64 zz = qz0 + qd1 * w1 + qd2 * w2;
                             const u32 zq = nr_quantize_depth_hw(zz);
                             const int kp = rr * KS + xx;
                             if (ZMODE == 1) atomicMin(&key[kp], ((u64)zq << 32) | fid);
