@@ -378,10 +378,12 @@ __device__ __forceinline__ void raster_stamp_end(const FrameParams& fp) {
 // Y of every pixel, U and V from the even pixel of each 2x2 block (tiles have
 // even sizes and origins, so a block never straddles two).
 // Output stores of the rasters' shading passes (framebuffer, depth, frame
-// output): written once per frame and not read again by the kernel (plain
-// stores; non-temporal ones were not faster, round 3).
+// output): written once per frame and not read again by the kernel, so
+// non-temporal (streaming) stores -- round 6, with the fast clear and the
+// binning beside the raster: C3 -2.5 %, an 8-way share -2.6 %, 1080p and C2
+// within 1 % (profiles/r06/ab_ntst.txt; round 3, frame outputs only: +-2 %).
 template <class T>
-__device__ __forceinline__ void out_store(T* p, T v) { *p = v; }
+__device__ __forceinline__ void out_store(T* p, T v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void store_frame_out(const FrameParams& fp, i64 p, i64 px, i64 py, f64 cr, f64 cg, f64 cb,
                                                 f64 ca) {
     if (!fp.frameU8) return;

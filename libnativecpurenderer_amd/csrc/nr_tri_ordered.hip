@@ -482,9 +482,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         const i64 py = y0 + lrow0 + r * SR;
         if (px < fp.W && py < fp.H) {
             f64* p = fp.fb + (py * fp.W + px) * ipp;
-            p[0] = cr[r]; p[1] = cg[r]; p[2] = cb[r];
-            if (RGBA) p[3] = ca[r];
-            if (DEPTH && (fp.depthWrite || fp.pendDepth)) fp.depth[py * fp.W + px] = cz[r];
+            out_store<f64>(p, cr[r]); out_store<f64>(p + 1, cg[r]); out_store<f64>(p + 2, cb[r]);
+            if (RGBA) out_store<f64>(p + 3, ca[r]);
+            if (DEPTH && (fp.depthWrite || fp.pendDepth)) out_store<u32>(fp.depth + py * fp.W + px, cz[r]);
             store_frame_out(fp, py * fp.W + px, px, py, cr[r], cg[r], cb[r], RGBA ? ca[r] : 1.0);
         }
     }
