@@ -102,7 +102,10 @@ def algorithmic_bytes(cfg, n_tri, frac=1.0, u8=True, frame_out="rgb"):
 # long: its clocks ramp for ~30 ms after idle, so a short run (the driver's
 # --warmup 5 --steps 20) would otherwise time part of the ramp (~3-6 %,
 # profiles/r04/warmup_steps20.txt).  Reported as "clock_settle" in the line.
-CLOCK_SETTLE_MS = 60.0
+# Round 6: 250 ms -- the C3 line at the driver's flags read 0.1293 ms (mean of 3)
+# after 60 ms and 0.1252 after 250 ms on the same box, each rep lower; 1000 ms no
+# better (profiles/r06/ab_settle.txt).
+CLOCK_SETTLE_MS = 250.0
 
 KERNEL_SYMBOL = {"tile_raster": "k_vis (order-free) / k_tile_raster (ordered)"}
 
