@@ -17,6 +17,9 @@ def main():
     settle = sys.argv[3] if len(sys.argv) > 3 else str(bench.CLOCK_SETTLE_MS)
     args = bench.parse_args(["--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-extra",
                              "--clock-settle-ms", settle])
+    if os.environ.get("PROBE_LIB"):   # a variant build (tools/exp/<name>.so)
+        from libnativecpurenderer_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(os.environ["PROBE_LIB"])
     import torch
     torch.cuda.set_device(0)
     from libnativecpurenderer_amd import libNativeCPURendererPybind as R
